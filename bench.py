@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of batched self-play on MI355X (BASELINE.json metric).
+
+Default workload = config 3: 1,048,576 random-policy games from the opening to
+terminal per GPU, one ``oth_rollout`` launch per bench step (each step plays a
+fresh range of global game ids), histogram all-reduced over ranks (config 4 at
+N>1, weak scaling).  value = env-steps (plies summed from the kernel's own
+histogram, passes included) of ALL ranks / max-over-ranks wall time.
+
+Also reported on rank 0 (secondary, same JSON line):
+  * step_65536 : config 2, one oth_step launch over 65,536 reachable mid-game
+    positions (52 algorithmic HBM bytes per step), repeated launches;
+  * step_steady: the same kernel over 16,777,216 positions (HBM roofline);
+  * greedy     : config 5, 1,048,576 1-ply greedy-mobility games;
+  * cpu_baseline: the C oracle (mailbox restatement of board.py) on a bounded
+    sample of the same workload on the host cores.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload rollout|greedy|step]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md
+STEP_BYTES = 52  # algorithmic bytes per oth_step: in 16+1+1, out 16+1+8+8+1
+ROLLOUT_BYTES_PER_GAME = 18  # final board 16 + diff 1 + plies 1 written; opening generated in-kernel
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", choices=["rollout", "greedy", "step"], default="rollout")
+    p.add_argument("--games", type=int, default=1 << 20, help="games per GPU per bench step (rollout workloads)")
+    p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--no-secondary", action="store_true", help="skip the secondary step/greedy/cpu measurements")
+    p.add_argument("--cpu-games", type=int, default=100000, help="bounded cpu_baseline sample (games)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from subproc_amd import ops
+    from subproc_amd._lib import HIST_BINS
+
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n = args.games
+    policy = "greedy" if args.workload == "greedy" else "random"
+    out = {}
+
+    if args.workload in ("rollout", "greedy"):
+        hists = torch.zeros((args.warmup + args.steps, HIST_BINS), dtype=torch.int64, device=dev)
+        fb = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        df = torch.empty(n, dtype=torch.int8, device=dev)
+        pl = torch.empty(n, dtype=torch.uint8, device=dev)
+        from subproc_amd import _lib
+
+        lib = _lib.load()
+        pid = 0 if policy == "random" else 1
+
+        def one_step(s):
+            # bench step s plays global game ids [(s*world + rank)*n, +n): fresh games every step
+            h = hists[s]
+            _lib.check(lib.oth_rollout(None, None, args.seed, (s * world + rank) * n, pid, 10, fb.data_ptr(),
+                                       df.data_ptr(), pl.data_ptr(), None, h.data_ptr(), n, stream.cuda_stream),
+                       "oth_rollout")
+            if world > 1:
+                dist.all_reduce(h, op=dist.ReduceOp.SUM)  # config 4: the one collective, inside the timed region
+
+        for s in range(args.warmup):
+            one_step(s)
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for s in range(args.warmup, args.warmup + args.steps):
+            one_step(s)
+        ev1.record(stream)
+        barrier()
+        t1 = time.perf_counter()
+        elapsed = max_over_ranks(t1 - t0)
+        kern_ms = ev0.elapsed_time(ev1) / args.steps  # stream-ordered: the rollout launch (+ all-reduce at N>1)
+        timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) at N>1
+        env_steps = int(timed[132])
+        games = n * world * args.steps
+        value = env_steps / elapsed
+        out.update(metric="env-steps/sec (batched self-play)", value=value, unit="env-steps/s",
+                   n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
+                   higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u64",
+                   data="synthetic (games from the opening, counter-based RNG seed %#x)" % args.seed,
+                   config={"workload": "config%d: %s-policy self-play rollouts to terminal" %
+                           (3 if policy == "random" and world == 1 else 4 if policy == "random" else 5, policy),
+                           "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
+                           "env_steps_per_game": env_steps / games})
+        per_launch_games = n
+        achieved = per_launch_games * ROLLOUT_BYTES_PER_GAME / (kern_ms * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                           "kernel": "rollout_kernel", "kernel_ms": kern_ms,
+                           "note": "integer-VALU-bound kernel: %d algorithmic B/game written; see valu figures in "
+                                   "DESIGN.md" % ROLLOUT_BYTES_PER_GAME}
+    else:
+        out.update(_bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks))
+
+    if world == 1 and not args.no_secondary:  # secondary + cpu_baseline: rank 0 at N=1 only
+        sec = {}
+        if args.workload != "step":
+            sec["step_65536"] = _bench_step(ops, torch, dev, stream, args, 65536, 1, torch.cuda.synchronize,
+                                            lambda x: x, launches=200)
+            sec["step_steady_16M"] = _bench_step(ops, torch, dev, stream, args, 1 << 24, 1, torch.cuda.synchronize,
+                                                 lambda x: x, launches=10)
+        if args.workload != "greedy":
+            sec["greedy_1M"] = _bench_greedy(ops, torch, dev, stream, args)
+        out["secondary"] = sec
+        out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks, launches=None):
+    """config 2: oth_step over n reachable mid-game positions (inputs resident in HBM)."""
+    from subproc_amd import _lib
+
+    lib = _lib.load()
+    pos = ops.sample_midgame(n, args.seed, index0=0, device=dev)
+    bo = torch.empty_like(pos.boards)
+    to = torch.empty_like(pos.turn)
+    fl = torch.empty(n, dtype=torch.int64, device=dev)
+    ln = torch.empty(n, dtype=torch.int64, device=dev)
+    rt = torch.empty(n, dtype=torch.int8, device=dev)
+    K = launches if launches is not None else args.steps
+    ptrs = (pos.boards.data_ptr(), pos.turn.data_ptr(), pos.move.data_ptr(), bo.data_ptr(), to.data_ptr(),
+            fl.data_ptr(), ln.data_ptr(), rt.data_ptr(), None, n, stream.cuda_stream)
+    for _ in range(max(3, args.warmup)):
+        _lib.check(lib.oth_step(*ptrs), "oth_step")
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(K):
+        _lib.check(lib.oth_step(*ptrs), "oth_step")
+    ev1.record(stream)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    kern_ms = ev0.elapsed_time(ev1) / K
+    steps = n * K * world
+    achieved = n * STEP_BYTES / (kern_ms * 1e-3) / 1e9
+    return {"metric": "env-steps/sec (batched step)", "value": steps / elapsed, "unit": "env-steps/s",
+            "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "step_kernel"}}
+
+
+def _bench_greedy(ops, torch, dev, stream, args):
+    n = args.games
+    hist = torch.zeros(133, dtype=torch.int64, device=dev)
+    ops.rollout(n // 16, args.seed, 0, "greedy", 10, hist=hist, device=dev, want_boards=False)
+    torch.cuda.synchronize()
+    hist.zero_()
+    t0 = time.perf_counter()
+    ops.rollout(n, args.seed, 1 << 40, "greedy", 10, hist=hist, device=dev)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "env-steps/sec (greedy-mobility self-play)", "value": int(hist[132]) / dt,
+            "unit": "env-steps/s", "games": n, "ms": dt * 1e3}
+
+
+def _cpu_baseline(args, workload):
+    """The C oracle (board.py restated as an 8x8 mailbox ray scan) on host cores."""
+    import oracle
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count()
+    threads = max(1, min(16, cores))
+    if workload == "step":
+        pos = oracle.sample_midgame(65536, args.seed)
+        t0 = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            oracle.step(pos["boards"], pos["turn"], pos["move"])
+        dt = time.perf_counter() - t0
+        return {"value": 65536 * reps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+                "sample": "%d x oracle_step over 65,536 mid-game positions" % reps}
+    games = args.cpu_games
+    pid = 0 if workload == "random" else 1
+    if pid == 1:
+        games = max(1000, games // 10)
+    t0 = time.perf_counter()
+    r = oracle.rollout(games, args.seed, 0, pid, 10, n_threads=threads)
+    dt = time.perf_counter() - t0
+    steps = int(r["hist"][132])
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d %s games from the opening (%d env-steps), C mailbox restatement of board.py, "
+                      "OpenMP %d threads, %.2f s wall" % (games, workload, steps, threads, dt),
+            "board_py_note": "board.py itself (Python) measured at ~2.9e3 env-steps/s/core in the build container "
+                             "(BASELINE.md); it cannot run on the GPU box"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,104 @@
+/*
+ * othello.h — C-ABI of the MI355X-native batched Othello environment
+ * (libsubproc_amd_hip.so, built from subproc_amd/csrc/othello.hip for gfx950).
+ *
+ * The reference (ysnrkdm/subproc) has no FFI: its step path is the Python
+ * class board.Board (board.py:20-262), imported as a module by
+ * game_runner.py:3, learn_base.py:1 and parameter.py:2.  Each entry point
+ * below is the batched replacement of one group of Board methods; the Python
+ * facade subproc_amd/board.py restores the exact method-level API on top of it
+ * (INTEGRATION.md shows the ctypes binding).
+ *
+ * Conventions:
+ *   board   = 2 x uint64 per game, [black, white] (colour-absolute), array (n,2)
+ *             bit sq = x + 8*y, x = file a..h, y = rank 1..8   (board.py:74-81)
+ *   turn    = uint8, 1 = Black, 2 = White                         (board.py:3-7)
+ *   move    = uint8 code, 0..63 = square, 64 = pass ('PS')      (board.py:192-209)
+ *   legal   = uint64 bitboard; LSB-first order == puttables() row-major order
+ *
+ * Ownership / errors / threading:
+ *   - every pointer is DEVICE memory owned by the caller (e.g. torch tensors);
+ *     the library allocates nothing persistent;
+ *   - calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
+ *     and thread-safe on distinct streams;
+ *   - return value: OTH_OK (0), OTH_EINVAL (invalid argument, nothing launched),
+ *     or -(hipError_t) of the failed launch.  Per-game semantics (illegal
+ *     move ...) are reported in `ret`, never as a status.
+ */
+#ifndef SUBPROC_AMD_OTHELLO_H
+#define SUBPROC_AMD_OTHELLO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OTH_OK 0
+#define OTH_EINVAL (-1000)
+
+#define OTH_BLACK 1
+#define OTH_WHITE 2
+#define OTH_PASS 64
+#define OTH_HIST_BINS 133   /* [0..128] diff+64, 129 black wins, 130 white wins, 131 draws, 132 total plies */
+#define OTH_MOVES_STRIDE 128 /* bytes per game in the optional rollout move record */
+
+#define OTH_POLICY_RANDOM 0
+#define OTH_POLICY_GREEDY 1  /* 1-ply minimise opponent mobility, ties -> lowest square */
+
+/* Library version string ("subproc_amd <semver> gfx950"). */
+const char* oth_version(void);
+
+/* Board.__init__ (board.py:22-27) for n games: opening position, turn = Black,
+ * nturn = 0.  turn / nturn may be NULL. */
+int oth_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n, void* stream);
+
+/* Board.puttables(turn) (board.py:46-52) as a bitmask per game;
+ * Board.n_puttable_for (54-55) = popcount.  turn outside {1,2} -> legal = 0. */
+int oth_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int64_t n, void* stream);
+
+/* Board.put_s (board.py:192-209) on integer move codes, one step per game:
+ *   move == 64            -> ret 0, turn toggles (accepted even with legal moves)
+ *   move 0..63, legal     -> ret = number of flipped discs (>= 1), board updated, turn toggles
+ *   move 0..63, occupied or flips nothing -> ret -1, board and turn unchanged
+ *   move > 64 or turn not in {1,2}         -> ret -1, unchanged  (board.py raises
+ *                                              IndexError for 'a9')
+ * Outputs: boards_out (n,2), turn_out, flips (discs flipped, origin excluded),
+ * legal_next = puttables(turn_out) on boards_out, ret.  Any output may be NULL.
+ * boards_out may alias boards_in and turn_out may alias turn_in (in-place step).
+ * nturn (may be NULL) is incremented in place where ret >= 0 (board.py:203-204). */
+int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* move,
+             uint64_t* boards_out, uint8_t* turn_out, uint64_t* flips, uint64_t* legal_next,
+             int8_t* ret, uint8_t* nturn, int64_t n, void* stream);
+
+/* n_black / n_white (board.py:37-41), diff = n_black - n_white (game_runner.py:194-199,
+ * no empty-square bonus), terminal = is_game_over() (board.py:57-58).  Any output may be NULL. */
+int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff,
+               uint8_t* terminal, int64_t n, void* stream);
+
+/* Play n independent games to terminal (game_runner.py:165-201 loop, engines
+ * replaced by `policy`; a side without a legal move passes).
+ *   start / start_turn : (n,2) / (n) start positions; NULL = opening, Black to move
+ *   seed, game_id0     : game i uses the RNG stream of global game id game_id0 + i
+ *                         -> results independent of batch split / GPU count
+ *   policy, n_random   : OTH_POLICY_RANDOM, or OTH_POLICY_GREEDY whose first
+ *                        n_random plies are random
+ * Outputs (each may be NULL): final_boards (n,2), diff (n), plies (n) = env-steps
+ * incl. passes, moves (n * OTH_MOVES_STRIDE, 255-padded move codes),
+ * hist (OTH_HIST_BINS int64, ACCUMULATED: caller zeroes it). */
+int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+
+/* Synthetic reachable mid-game positions for the step benchmark (config 2):
+ * position index0+j is a random-policy playout of 10..49 plies from the opening
+ * at which the mover has >= 1 legal move, plus that mover's random legal move
+ * (DESIGN.md §Synthetic mid-game positions).  nturn may be NULL. */
+int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn,
+                       uint8_t* nturn, uint8_t* move, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SUBPROC_AMD_OTHELLO_H */

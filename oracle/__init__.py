@@ -1,0 +1,126 @@
+"""ctypes wrapper of the C parity oracle (oracle/othello_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — to be imported by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg as the *checker*; the product package
+subproc_amd/ never imports it.  numpy in / numpy out, host memory only.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+HIST_BINS = 133
+MOVES_STRIDE = 128
+
+_lib = None
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, I64, U64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
+        L.oracle_reset.argtypes = [P, P, P, I64]
+        L.oracle_legal.argtypes = [P, P, P, I64]
+        L.oracle_step.argtypes = [P, P, P, P, P, P, P, P, P, I64]
+        L.oracle_result.argtypes = [P, P, P, P, P, I64]
+        L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I]
+        L.oracle_sample_midgame.argtypes = [U64, U64, P, P, P, P, I64]
+        L.oracle_game_key.argtypes = [U64, U64]
+        L.oracle_game_key.restype = U64
+        L.oracle_ply_rand.argtypes = [U64, ctypes.c_uint32]
+        L.oracle_ply_rand.restype = ctypes.c_uint32
+        for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
+                  "oracle_sample_midgame"):
+            getattr(L, f).restype = I
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _boards(b):
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    assert b.ndim == 2 and b.shape[1] == 2
+    return b
+
+
+def reset(n):
+    b = np.empty((n, 2), np.uint64)
+    t = np.empty(n, np.uint8)
+    nt = np.empty(n, np.uint8)
+    lib().oracle_reset(_p(b), _p(t), _p(nt), n)
+    return b, t, nt
+
+
+def legal(boards, turn):
+    boards = _boards(boards)
+    turn = np.ascontiguousarray(turn, np.uint8)
+    out = np.empty(len(boards), np.uint64)
+    lib().oracle_legal(_p(boards), _p(turn), _p(out), len(boards))
+    return out
+
+
+def step(boards, turn, move, nturn=None):
+    boards = _boards(boards)
+    n = len(boards)
+    turn = np.ascontiguousarray(turn, np.uint8)
+    move = np.ascontiguousarray(move, np.uint8)
+    bo = np.empty((n, 2), np.uint64)
+    to = np.empty(n, np.uint8)
+    fl = np.empty(n, np.uint64)
+    ln = np.empty(n, np.uint64)
+    r = np.empty(n, np.int8)
+    nt = None if nturn is None else np.array(nturn, np.uint8)
+    lib().oracle_step(_p(boards), _p(turn), _p(move), _p(bo), _p(to), _p(fl), _p(ln), _p(r), _p(nt), n)
+    return dict(boards=bo, turn=to, flips=fl, legal_next=ln, ret=r, nturn=nt)
+
+
+def result(boards):
+    boards = _boards(boards)
+    n = len(boards)
+    nb, nw, t = (np.empty(n, np.uint8) for _ in range(3))
+    d = np.empty(n, np.int8)
+    lib().oracle_result(_p(boards), _p(nb), _p(nw), _p(d), _p(t), n)
+    return dict(n_black=nb, n_white=nw, diff=d, terminal=t)
+
+
+def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=None, record_moves=False,
+            n_threads=0):
+    start = None if start is None else _boards(start)
+    st = None if start_turn is None else np.ascontiguousarray(start_turn, np.uint8)
+    fb = np.empty((n, 2), np.uint64)
+    d = np.empty(n, np.int8)
+    pl = np.empty(n, np.uint8)
+    mv = np.empty((n, MOVES_STRIDE), np.uint8) if record_moves else None
+    h = np.zeros(HIST_BINS, np.int64)
+    lib().oracle_rollout(_p(start), _p(st), seed, game_id0, policy, n_random, _p(fb), _p(d), _p(pl), _p(mv), _p(h),
+                         n, n_threads)
+    return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h)
+
+
+def sample_midgame(n, seed, index0=0):
+    b = np.empty((n, 2), np.uint64)
+    t, nt, m = (np.empty(n, np.uint8) for _ in range(3))
+    lib().oracle_sample_midgame(seed, index0, _p(b), _p(t), _p(nt), _p(m), n)
+    return dict(boards=b, turn=t, nturn=nt, move=m)
+
+
+def game_key(seed, g):
+    return lib().oracle_game_key(seed, g)
+
+
+def ply_rand(key, ply):
+    return lib().oracle_ply_rand(key, ply)

@@ -1,0 +1,370 @@
+/*
+ * othello_oracle.c — CPU restatement of ysnrkdm/subproc board.py (the parity
+ * ORACLE).  TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg, never by the product path (subproc_amd/).
+ *
+ * Pinned against the reference: tests/test_oracle.py checks every function here
+ * against tests/golden/*, which tests/golden/gen_golden.py produced by running
+ * the real /root/reference/board.py (SURVEY.md §8c shim).
+ *
+ * Deliberately NOT a bitboard implementation: it follows board.py's own
+ * algorithm — an 8x8 mailbox ``board[y][x]`` scanned ray by ray from every
+ * cell — so the GPU's Kogge-Stone bitboards are checked against an independent
+ * formulation.  Bitboards appear only at the API boundary (sq = x + 8*y,
+ * SURVEY.md §8 conventions: board.py:74-81 mask_count defines the bit order).
+ *
+ * API mirrors include/othello.h with host pointers, prefix ``oracle_`` and no
+ * stream argument.
+ */
+#include <stdint.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { Empty = 0, Black = 1, White = 2 };  /* board.py:3-7 */
+#define PASS_CODE 64
+#define HIST_BINS 133
+#define MOVES_STRIDE 128
+
+/* DIRECS, board.py:9-17 — order LU, U, RU, L, R, LD, D, RD */
+static const int DIRECS[8][2] = {{-1, -1}, {0, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {0, 1}, {1, 1}};
+
+typedef struct {
+    int8_t b[8][8]; /* board[y][x], board.py:23 */
+    int turn;       /* board.py:26 */
+    int nturn;      /* board.py:27 */
+} Board;
+
+/* board.py:265-266 */
+static int is_within_board(int x, int y) { return 0 <= x && x < 8 && 0 <= y && y < 8; }
+
+/* board.py:155-159 */
+static int hostile(int piece) { return piece == Black ? White : Black; }
+
+/* board.py:22-27 */
+static void board_init(Board* s) {
+    memset(s->b, Empty, sizeof s->b);
+    s->b[3][3] = s->b[4][4] = White;
+    s->b[3][4] = s->b[4][3] = Black;
+    s->turn = Black;
+    s->nturn = 0;
+}
+
+static void board_from_bits(Board* s, uint64_t bl, uint64_t wh, int turn) {
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            int sq = x + 8 * y;
+            s->b[y][x] = (bl >> sq & 1) ? Black : (wh >> sq & 1) ? White : Empty;
+        }
+    s->turn = turn;
+    s->nturn = 0;
+}
+
+static void board_to_bits(const Board* s, uint64_t* bl, uint64_t* wh) {
+    uint64_t B = 0, W = 0;
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            if (s->b[y][x] == Black) B |= 1ull << (x + 8 * y);
+            else if (s->b[y][x] == White) W |= 1ull << (x + 8 * y);
+        }
+    *bl = B;
+    *wh = W;
+}
+
+/* hands_for_direc, board.py:124-139: hostile discs along one ray that end in
+ * an own disc; empty/edge discards the ray.  Writes squares to out, returns count. */
+static int hands_for_direc(const Board* s, int d, int piece, int x, int y, int out[8][2]) {
+    int n = 0, h = hostile(piece);
+    for (int i = 1; i < 9; i++) {
+        int nx = x + i * DIRECS[d][0], ny = y + i * DIRECS[d][1];
+        if (is_within_board(nx, ny) && s->b[ny][nx] == h) {
+            out[n][0] = nx;
+            out[n][1] = ny;
+            n++;
+        } else if (is_within_board(nx, ny) && s->b[ny][nx] == piece) {
+            break;
+        } else {
+            n = 0;
+            break;
+        }
+    }
+    return n;
+}
+
+/* is_puttable_at, board.py:141-149 */
+static int is_puttable_at(const Board* s, int piece, int x, int y) {
+    if (s->b[y][x] != Empty) return 0;
+    int tmp[8][2], n = 0;
+    for (int d = 0; d < 8; d++) n += hands_for_direc(s, d, piece, x, y, tmp);
+    return n > 0;
+}
+
+/* puttables, board.py:46-52, as a bitmask; row-major scan order == LSB-first */
+static uint64_t puttables(const Board* s, int piece) {
+    uint64_t m = 0;
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++)
+            if (is_puttable_at(s, piece, x, y)) m |= 1ull << (x + 8 * y);
+    return m;
+}
+
+static int popcount64(uint64_t m) { return __builtin_popcountll(m); }
+
+/* n_puttable_for, board.py:54-55 */
+static int n_puttable_for(const Board* s, int piece) { return popcount64(puttables(s, piece)); }
+
+/* is_game_over, board.py:57-58 (short-circuit kept) */
+static int is_game_over(const Board* s) { return n_puttable_for(s, Black) == 0 && n_puttable_for(s, White) == 0; }
+
+/* put, board.py:161-174: returns total flipped count, 0 = illegal (no change) */
+static int put(Board* s, int piece, int x, int y) {
+    if (s->b[y][x] != Empty) return 0;
+    int count = 0, hands[8][2];
+    for (int d = 0; d < 8; d++) {
+        int n = hands_for_direc(s, d, piece, x, y, hands);
+        if (n) {
+            for (int k = 0; k < n; k++) s->b[hands[k][1]][hands[k][0]] = (int8_t)piece; /* set_hands 151-153 */
+            count += n;
+            s->b[y][x] = (int8_t)piece;
+        }
+    }
+    return count;
+}
+
+/* put_s, board.py:192-209, on the integer move code (0..63 = x+8y, 64 = 'PS').
+ * Codes > 64 correspond to no string board.py accepts without IndexError;
+ * the C-ABI contract returns -1 for them. */
+static int put_code(Board* s, int code) {
+    int out = -1;
+    if (code == PASS_CODE) {
+        out = 0;
+    } else if (code >= 0 && code < 64) {
+        out = put(s, s->turn, code % 8, code / 8);
+        if (out == 0) out = -1;
+    }
+    if (out >= 0) {
+        s->nturn += 1;
+        s->turn = (s->turn == Black) ? White : Black;
+    }
+    return out;
+}
+
+static int n_of(const Board* s, int c) {
+    int n = 0; /* count_over_board, board.py:29-44 */
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) n += s->b[y][x] == c;
+    return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* RNG spec (Python twin in tests/golden/gen_golden.py)      */
+/* ------------------------------------------------------------------------ */
+#define GOLDEN64 0x9E3779B97F4A7C15ull
+static uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+static uint64_t seed_state(uint64_t seed) { return mix64(seed + GOLDEN64); }
+static uint64_t game_key(uint64_t S, uint64_t g) { return mix64(S + g * GOLDEN64); }
+static uint32_t ply_rand(uint64_t key, uint32_t ply) {
+    return mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + ply));
+}
+static int pick(uint64_t key, uint32_t ply, int n) { return (int)(((uint64_t)ply_rand(key, ply) * (uint64_t)n) >> 32); }
+
+/* k-th entry of puttables() (row-major list), as a square code */
+static int kth_square(uint64_t legal, int k) {
+    for (int sq = 0; sq < 64; sq++)
+        if (legal >> sq & 1) {
+            if (k == 0) return sq;
+            k--;
+        }
+    return -1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* exported API                                                             */
+/* ------------------------------------------------------------------------ */
+int oracle_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n) {
+    Board s;
+    board_init(&s);
+    uint64_t bl, wh;
+    board_to_bits(&s, &bl, &wh);
+    for (int64_t i = 0; i < n; i++) {
+        boards[2 * i] = bl;
+        boards[2 * i + 1] = wh;
+        if (turn) turn[i] = (uint8_t)s.turn;
+        if (nturn) nturn[i] = (uint8_t)s.nturn;
+    }
+    return 0;
+}
+
+int oracle_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int64_t n) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        board_from_bits(&s, boards[2 * i], boards[2 * i + 1], turn[i]);
+        legal[i] = (turn[i] == Black || turn[i] == White) ? puttables(&s, turn[i]) : 0;
+    }
+    return 0;
+}
+
+int oracle_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* move, uint64_t* boards_out,
+                uint8_t* turn_out, uint64_t* flips, uint64_t* legal_next, int8_t* ret, uint8_t* nturn, int64_t n) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        uint64_t b0 = boards_in[2 * i], w0 = boards_in[2 * i + 1];
+        int t = turn_in[i];
+        board_from_bits(&s, b0, w0, t);
+        int r = -1;
+        if (t == Black || t == White) r = put_code(&s, move[i]);
+        uint64_t bl, wh;
+        board_to_bits(&s, &bl, &wh);
+        if (boards_out) {
+            boards_out[2 * i] = bl;
+            boards_out[2 * i + 1] = wh;
+        }
+        if (turn_out) turn_out[i] = (uint8_t)s.turn;
+        /* flipped discs = opponent discs that changed colour (origin excluded) */
+        if (flips) flips[i] = (t == Black) ? (w0 & ~wh) : (t == White) ? (b0 & ~bl) : 0;
+        if (legal_next) legal_next[i] = (s.turn == Black || s.turn == White) ? puttables(&s, s.turn) : 0;
+        if (ret) ret[i] = (int8_t)r;
+        if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1); /* board.py:203-204 */
+    }
+    return 0;
+}
+
+int oracle_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff, uint8_t* terminal,
+                  int64_t n) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        board_from_bits(&s, boards[2 * i], boards[2 * i + 1], Black);
+        int nb = n_of(&s, Black), nw = n_of(&s, White);
+        if (n_black) n_black[i] = (uint8_t)nb;
+        if (n_white) n_white[i] = (uint8_t)nw;
+        if (diff) diff[i] = (int8_t)(nb - nw); /* game_runner.py:194-199 rule, no empty bonus */
+        if (terminal) terminal[i] = (uint8_t)is_game_over(&s);
+    }
+    return 0;
+}
+
+/* One game to terminal from s, game_runner.py:165-201 loop with the build's
+ * policies: a side with no move passes ('PS'). */
+static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* moves) {
+    int ply = 0;
+    while (!is_game_over(s)) {
+        uint64_t legal = puttables(s, s->turn);
+        int code;
+        if (!legal) {
+            code = PASS_CODE;
+        } else if (policy == 0 || ply < n_random) {
+            code = kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal)));
+        } else {
+            int best = -1, bestv = 1 << 30;
+            for (int sq = 0; sq < 64; sq++) {
+                if (!(legal >> sq & 1)) continue;
+                Board c = *s;
+                put_code(&c, sq);
+                int v = n_puttable_for(&c, hostile(s->turn));
+                if (v < bestv) { bestv = v; best = sq; }
+            }
+            code = best;
+        }
+        int r = put_code(s, code);
+        (void)r;
+        if (moves && ply < MOVES_STRIDE) moves[ply] = (uint8_t)code;
+        ply++;
+    }
+    return ply;
+}
+
+int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                   int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
+                   int64_t* hist, int64_t n, int n_threads) {
+    uint64_t S = seed_state(seed);
+    int64_t h[HIST_BINS];
+    memset(h, 0, sizeof h);
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel num_threads(n_threads)
+#endif
+    {
+        int64_t hl[HIST_BINS];
+        memset(hl, 0, sizeof hl);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = 0; i < n; i++) {
+            Board s;
+            if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
+            else board_init(&s);
+            if (moves) memset(moves + i * MOVES_STRIDE, 255, MOVES_STRIDE);
+            int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random,
+                              moves ? moves + i * MOVES_STRIDE : 0);
+            int d = n_of(&s, Black) - n_of(&s, White);
+            uint64_t bl, wh;
+            board_to_bits(&s, &bl, &wh);
+            if (final_boards) {
+                final_boards[2 * i] = bl;
+                final_boards[2 * i + 1] = wh;
+            }
+            if (diff) diff[i] = (int8_t)d;
+            if (plies) plies[i] = (uint8_t)p;
+            hl[d + 64]++;
+            hl[d > 0 ? 129 : d < 0 ? 130 : 131]++;
+            hl[132] += p;
+        }
+#pragma omp critical
+        for (int k = 0; k < HIST_BINS; k++) h[k] += hl[k];
+    }
+    if (hist)
+        for (int k = 0; k < HIST_BINS; k++) hist[k] += h[k];
+    return 0;
+}
+
+/* Synthetic mid-game position generator for the config-2 step benchmark
+ * (DESIGN.md §Synthetic mid-game positions; Python twin in gen_golden.py). */
+int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
+                          uint8_t* move, int64_t n) {
+    uint64_t S = seed_state(seed);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t j = 0; j < n; j++) {
+        uint64_t i = index0 + (uint64_t)j;
+        for (uint64_t attempt = 0;; attempt++) {
+            uint64_t key = game_key(S, i ^ (attempt << 48));
+            int target = 10 + pick(key, 200, 40);
+            Board s;
+            board_init(&s);
+            int ply = 0, ok = 0;
+            while (!is_game_over(&s)) {
+                uint64_t legal = puttables(&s, s.turn);
+                if (ply >= target && legal) { ok = 1; break; }
+                int code = legal ? kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal))) : PASS_CODE;
+                put_code(&s, code);
+                ply++;
+            }
+            if (ok) {
+                uint64_t legal = puttables(&s, s.turn);
+                board_to_bits(&s, &boards[2 * j], &boards[2 * j + 1]);
+                turn[j] = (uint8_t)s.turn;
+                if (nturn) nturn[j] = (uint8_t)ply;
+                move[j] = (uint8_t)kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal)));
+                break;
+            }
+        }
+    }
+    return 0;
+}
+
+/* RNG known answers for the fixture check */
+uint64_t oracle_game_key(uint64_t seed, uint64_t g) { return game_key(seed_state(seed), g); }
+uint32_t oracle_ply_rand(uint64_t key, uint32_t ply) { return ply_rand(key, ply); }

@@ -1,0 +1,62 @@
+"""Multi-GPU self-play: one process per GPU, disjoint global game-id ranges,
+ONE all_reduce(SUM) of the int64[133] win/score histogram (RCCL over xGMI with
+backend "nccl"; gloo for CPU tests).
+
+Replaces the reference's job fan-out (Resque/pyres queues on Redis,
+replearn.py:78-86 -> eljem_worker.py:10 -> subproc.do_match) for the env path:
+games are independent, so there is no data-path collective; the only exchange
+is the episode-count/score reduction.
+"""
+import torch
+import torch.distributed as dist
+
+from ._lib import HIST_BINS
+
+
+def shard_range(total, rank, world):
+    """Contiguous [begin, end) of `total` games for `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(total, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None, rollout_fn=None, device=None,
+                    game_id_base=0):
+    """Play `total_games` games split over the ranks of `group`; returns
+    (global histogram int64[133] on every rank, local game count).
+
+    Game g (global id game_id_base + g) always uses the same RNG stream, so the
+    reduced histogram is identical for any world size (bit-exact check of the
+    all-reduce path: tests/test_dist.py).  `rollout_fn(n, seed, game_id0,
+    policy, n_random, hist)` defaults to the HIP kernel (subproc_amd.ops.rollout).
+    """
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    begin, end = shard_range(total_games, rank, world)
+    if rollout_fn is None:
+        from . import ops
+
+        def rollout_fn(n, seed, game_id0, policy, n_random, hist):
+            ops.rollout(n, seed, game_id0, policy, n_random, hist=hist, device=hist.device, want_boards=False,
+                        want_diff=False, want_plies=False)
+
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+    hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=device)
+    if end > begin:
+        rollout_fn(end - begin, seed, game_id_base + begin, policy, n_random, hist)
+    if world > 1:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    return hist, end - begin
+
+
+def hist_summary(hist):
+    """Batch statistics from the histogram (learn_base.py:58-109 quantities,
+    with the correct white-win rule, not learn_base.py:77's comparison bug)."""
+    h = hist.tolist() if isinstance(hist, torch.Tensor) else list(hist)
+    games = sum(h[:129])
+    diffs = [d - 64 for d in range(129) if h[d]]
+    return dict(games=games, black_wins=h[129], white_wins=h[130], draws=h[131], plies=h[132],
+                black_win_rate=h[129] / games if games else 0.0, white_win_rate=h[130] / games if games else 0.0,
+                avg_diff=sum((d - 64) * h[d] for d in range(129)) / games if games else 0.0,
+                min_diff=min(diffs) if diffs else 0, max_diff=max(diffs) if diffs else 0)

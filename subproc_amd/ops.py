@@ -1,0 +1,203 @@
+"""Tensor-level batched Othello ops on the MI355X (one call = one HIP launch).
+
+Every function takes/returns torch tensors resident on a ROCm device and calls
+the C-ABI of include/othello.h on torch's current stream.  Bitboards are
+``(n, 2)`` ``torch.int64`` tensors holding the uint64 bit patterns
+``[black, white]`` (torch has no general uint64 arithmetic; the bits are what
+matter, see :func:`to_numpy_u64`).  There is no CPU fallback: CPU tensors or a
+missing library raise.
+
+Reference mapping (board.py line numbers):
+  reset   -> Board.__init__            22-27
+  legal   -> Board.puttables           46-52   (n_puttable_for = popcount)
+  step    -> Board.put_s / put         161-209
+  result  -> n_black / n_white / is_game_over 37-58 + game_runner.py:194-199
+  rollout -> GameRunner.play_a_game loop   game_runner.py:165-201
+"""
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import BLACK, HIST_BINS, MOVES_STRIDE, PASS, POLICY_GREEDY, POLICY_RANDOM, WHITE, check
+
+StepResult = namedtuple("StepResult", "boards turn flips legal_next ret")
+Result = namedtuple("Result", "n_black n_white diff terminal")
+RolloutResult = namedtuple("RolloutResult", "final_boards diff plies moves hist")
+Positions = namedtuple("Positions", "boards turn nturn move")
+
+_POLICIES = {"random": POLICY_RANDOM, "greedy": POLICY_GREEDY, POLICY_RANDOM: POLICY_RANDOM,
+             POLICY_GREEDY: POLICY_GREEDY}
+
+
+def _stream():
+    return ctypes_stream(torch.cuda.current_stream())
+
+
+def ctypes_stream(s):
+    return s.cuda_stream  # hipStream_t as an integer handle
+
+
+def _dev(t, name, dtype, shape=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: tensor must be on a ROCm device (got {t.device}); there is no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    return t.data_ptr()
+
+
+def _opt(t, name, dtype, shape):
+    return None if t is None else _dev(t, name, dtype, shape)
+
+
+def _n(boards):
+    if boards.dim() != 2 or boards.shape[1] != 2:
+        raise ValueError(f"boards: expected shape (n, 2), got {tuple(boards.shape)}")
+    return boards.shape[0]
+
+
+def _device(device):
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"device must be a ROCm device, got {d}")
+    return d
+
+
+# ---------------------------------------------------------------------------
+def reset(n, device="cuda"):
+    """n games at the opening position: (boards (n,2) int64, turn (n,) uint8, nturn (n,) uint8)."""
+    d = _device(device)
+    boards = torch.empty((n, 2), dtype=torch.int64, device=d)
+    turn = torch.empty(n, dtype=torch.uint8, device=d)
+    nturn = torch.empty(n, dtype=torch.uint8, device=d)
+    with torch.cuda.device(d):
+        check(_lib.load().oth_reset(boards.data_ptr(), turn.data_ptr(), nturn.data_ptr(), n, _stream()), "oth_reset")
+    return boards, turn, nturn
+
+
+def legal(boards, turn, out=None):
+    """Legal-move bitboard of the side to move (Board.puttables as a mask)."""
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    pt = _dev(turn, "turn", torch.uint8, (n,))
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=boards.device)
+    po = _dev(out, "out", torch.int64, (n,))
+    with torch.cuda.device(boards.device):
+        check(_lib.load().oth_legal(pb, pt, po, n, _stream()), "oth_legal")
+    return out
+
+
+def step(boards, turn, move, nturn=None, inplace=False, want_flips=True, want_legal=True):
+    """One Board.put_s per game on integer move codes (0..63 square, 64 pass).
+
+    Returns StepResult(boards, turn, flips, legal_next, ret) with ret exactly as
+    board.py: -1 illegal (state unchanged), 0 pass, n >= 1 discs flipped.
+    ``nturn`` (uint8, optional) is incremented in place where ret >= 0.
+    ``inplace=True`` writes the new boards/turn into the input tensors.
+    """
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    pt = _dev(turn, "turn", torch.uint8, (n,))
+    pm = _dev(move, "move", torch.uint8, (n,))
+    pn = _opt(nturn, "nturn", torch.uint8, (n,))
+    dev = boards.device
+    bo = boards if inplace else torch.empty_like(boards)
+    to = turn if inplace else torch.empty_like(turn)
+    fl = torch.empty(n, dtype=torch.int64, device=dev) if want_flips else None
+    ln = torch.empty(n, dtype=torch.int64, device=dev) if want_legal else None
+    ret = torch.empty(n, dtype=torch.int8, device=dev)
+    with torch.cuda.device(dev):
+        check(_lib.load().oth_step(pb, pt, pm, bo.data_ptr(), to.data_ptr(), None if fl is None else fl.data_ptr(),
+                                   None if ln is None else ln.data_ptr(), ret.data_ptr(), pn, n, _stream()),
+              "oth_step")
+    return StepResult(bo, to, fl, ln, ret)
+
+
+def result(boards):
+    """Result(n_black, n_white, diff = n_black - n_white, terminal = is_game_over())."""
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    dev = boards.device
+    nb = torch.empty(n, dtype=torch.uint8, device=dev)
+    nw = torch.empty(n, dtype=torch.uint8, device=dev)
+    df = torch.empty(n, dtype=torch.int8, device=dev)
+    te = torch.empty(n, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        check(_lib.load().oth_result(pb, nb.data_ptr(), nw.data_ptr(), df.data_ptr(), te.data_ptr(), n, _stream()),
+              "oth_result")
+    return Result(nb, nw, df, te)
+
+
+def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start_turn=None, record_moves=False,
+            hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True):
+    """Play n games to terminal on the GPU (one lane per game).
+
+    Game i uses the RNG stream of global id game_id0 + i, so results do not
+    depend on how games are split over launches or GPUs.  ``hist`` (int64[133])
+    is accumulated into if given (zero it yourself), else a fresh zeroed one is
+    returned: [0..128] diff+64, 129 black wins, 130 white wins, 131 draws,
+    132 total plies (= env-steps).
+    """
+    if policy not in _POLICIES:
+        raise ValueError(f"policy must be 'random' or 'greedy', got {policy!r}")
+    d = _device(device) if start is None else start.device
+    ps = pst = None
+    if start is not None:
+        if _n(start) != n:
+            raise ValueError("start must have n rows")
+        ps = _dev(start, "start", torch.int64)
+        pst = _opt(start_turn, "start_turn", torch.uint8, (n,))
+    fb = torch.empty((n, 2), dtype=torch.int64, device=d) if want_boards else None
+    df = torch.empty(n, dtype=torch.int8, device=d) if want_diff else None
+    pl = torch.empty(n, dtype=torch.uint8, device=d) if want_plies else None
+    mv = torch.empty((n, MOVES_STRIDE), dtype=torch.uint8, device=d) if record_moves else None
+    if hist is None:
+        hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=d)
+    ph = _dev(hist, "hist", torch.int64, (HIST_BINS,))
+
+    def ptr(t):
+        return None if t is None else t.data_ptr()
+
+    with torch.cuda.device(d):
+        check(_lib.load().oth_rollout(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy], n_random, ptr(fb),
+                                      ptr(df), ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout")
+    return RolloutResult(fb, df, pl, mv, hist)
+
+
+def sample_midgame(n, seed, index0=0, device="cuda"):
+    """Synthetic reachable mid-game positions + one random legal move each (config 2 inputs)."""
+    d = _device(device)
+    b = torch.empty((n, 2), dtype=torch.int64, device=d)
+    t = torch.empty(n, dtype=torch.uint8, device=d)
+    nt = torch.empty(n, dtype=torch.uint8, device=d)
+    m = torch.empty(n, dtype=torch.uint8, device=d)
+    with torch.cuda.device(d):
+        check(_lib.load().oth_sample_midgame(seed & (2**64 - 1), index0, b.data_ptr(), t.data_ptr(), nt.data_ptr(),
+                                             m.data_ptr(), n, _stream()), "oth_sample_midgame")
+    return Positions(b, t, nt, m)
+
+
+# ---------------------------------------------------------------------------
+# host <-> device conversion helpers (uint64 bit patterns)
+# ---------------------------------------------------------------------------
+def to_numpy_u64(t):
+    """Device/host int64 tensor -> numpy uint64 array with the same bits."""
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def from_numpy_u64(a, device="cuda"):
+    """numpy uint64 array -> int64 tensor with the same bits on `device`."""
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return torch.from_numpy(a.view(np.int64).copy()).to(device)
+
+
+__all__ = ["reset", "legal", "step", "result", "rollout", "sample_midgame", "to_numpy_u64", "from_numpy_u64",
+           "StepResult", "Result", "RolloutResult", "Positions", "BLACK", "WHITE", "PASS", "HIST_BINS"]

@@ -1,0 +1,380 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REAL reference board.py.
+
+TEST INFRASTRUCTURE ONLY.  Runs in the build container only (never on the GPU
+box): it needs /root/reference/board.py and refuses to run without it.
+
+How the reference is loaded: board.py is Python 2 but only two
+lines are not valid Python 3, so its text is read, exactly two substitutions are
+applied in memory, and the result is exec'd into a private namespace:
+  * board.py:92  ``print q``  -> ``print(q)``      (display-only show_mask)
+  * board.py:257 ``i / 8``    -> ``i // 8``        (deserialize row index)
+Nothing is written to /root/reference and no reference source is copied into
+this repository; only inputs/outputs (data) are committed.
+
+The move-selection rule for rollouts is OUR spec (board.py has no RNG; the
+reference picks with Python's ``random.randrange`` in game_runner.py:133-152).
+The spec is restated here in pure Python and every trajectory is driven through
+board.py's own ``puttables`` / ``put_s`` / ``is_game_over`` so the fixtures pin
+(board, move) -> next state semantics to the reference, and the RNG spec to a
+second independent implementation.
+
+Usage:  python tests/golden/gen_golden.py        (≈1–2 min on 8 cores)
+"""
+import json
+import multiprocessing as mp
+import os
+import sys
+
+import numpy as np
+
+REF = "/root/reference/board.py"
+OUT = os.path.dirname(os.path.abspath(__file__))
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+GOLDEN64 = 0x9E3779B97F4A7C15
+PASS = 64
+SEED = 0x5EED
+
+
+# ----------------------------------------------------------------------------
+# reference loader (the shim of SURVEY.md §8c)
+# ----------------------------------------------------------------------------
+def load_reference_board():
+    if not os.path.exists(REF):
+        sys.exit("gen_golden.py: /root/reference/board.py absent - fixtures can only be generated in the build container")
+    src = open(REF).read()
+    a, b = "        print q\n", "i % 8, i / 8)"
+    assert src.count(a) == 1 and src.count(b) == 1, "board.py changed; shim substitutions no longer apply"
+    src = src.replace(a, "        print(q)\n").replace(b, "i % 8, i // 8)")
+    ns = {"__name__": "reference_board"}
+    exec(compile(src, "reference_board.py", "exec"), ns)
+    return ns
+
+
+RB = load_reference_board()
+Board = RB["Board"]
+Black, White, Empty = RB["Black"], RB["White"], RB["Empty"]
+
+
+# ----------------------------------------------------------------------------
+# helpers: reference Board <-> bitboards (sq = x + 8*y, SURVEY.md §8 conventions)
+# ----------------------------------------------------------------------------
+def to_bits(b):
+    bl = wh = 0
+    for y in range(8):
+        for x in range(8):
+            c = b.get(x, y)
+            if c == Black:
+                bl |= 1 << (x + 8 * y)
+            elif c == White:
+                wh |= 1 << (x + 8 * y)
+    return bl, wh
+
+
+def from_bits(bl, wh, turn, nturn=0):
+    b = Board()
+    for y in range(8):
+        for x in range(8):
+            sq = x + 8 * y
+            b.set(Black if bl >> sq & 1 else White if wh >> sq & 1 else Empty, x, y)
+    b.turn = turn
+    b.nturn = nturn
+    return b
+
+
+def clone(b):
+    c = Board()
+    c.board = [row[:] for row in b.board]
+    c.turn, c.nturn = b.turn, b.nturn
+    return c
+
+
+def legal_bits(b, piece):
+    m = 0
+    for (x, y) in b.puttables(piece):
+        m |= 1 << (x + 8 * y)
+    return m
+
+
+def code_to_str(b, code):
+    return "ps" if code == PASS else b.handstr_from_coord(code % 8, code // 8)
+
+
+def hostile(t):
+    return White if t == Black else Black
+
+
+# ----------------------------------------------------------------------------
+# RNG spec — pure-Python restatement
+# ----------------------------------------------------------------------------
+def mix64(z):
+    z &= M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def mix32(x):
+    x &= M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M32
+    x ^= x >> 16
+    return x
+
+
+def seed_state(seed):
+    return mix64((seed + GOLDEN64) & M64)
+
+
+def game_key(S, g):
+    return mix64((S + g * GOLDEN64) & M64)
+
+
+def ply_rand(key, ply):
+    return mix32((key & M32) ^ mix32(((key >> 32) + ply) & M32))
+
+
+def pick(key, ply, n):
+    return (ply_rand(key, ply) * n) >> 32
+
+
+# ----------------------------------------------------------------------------
+# trajectories driven through board.py
+# ----------------------------------------------------------------------------
+def play(args):
+    """One game from (bl, wh, turn) to terminal via board.py.
+
+    policy 0 = random (k-th legal square, LSB-first == puttables order);
+    policy 1 = greedy: for ply >= n_random pick the legal move minimising the
+    opponent's n_puttable_for on the child, ties -> first in puttables order.
+    A side with no legal move passes ('ps'), as the engines do in game_runner.
+    """
+    seed, g, policy, n_random, bl, wh, turn = args
+    key = game_key(seed_state(seed), g)
+    b = from_bits(bl, wh, turn)
+    moves = []
+    ply = 0
+    while not b.is_game_over():
+        puts = b.puttables(b.turn)
+        if not puts:
+            code = PASS
+        elif policy == 0 or ply < n_random:
+            x, y = puts[pick(key, ply, len(puts))]
+            code = x + 8 * y
+        else:
+            best, bestv = None, None
+            for (x, y) in puts:
+                c = clone(b)
+                assert c.put_s(c.handstr_from_coord(x, y)) > 0
+                v = c.n_puttable_for(hostile(b.turn))
+                if bestv is None or v < bestv:
+                    best, bestv = x + 8 * y, v
+            code = best
+        r = b.put_s(code_to_str(b, code))
+        assert r >= 0
+        moves.append(code)
+        ply += 1
+    fb, fw = to_bits(b)
+    return moves, fb, fw, b.n_black() - b.n_white(), ply
+
+
+def sample_midgame(args):
+    """Config-2 input generator spec: see DESIGN.md §Synthetic mid-game positions."""
+    seed, i = args
+    S = seed_state(seed)
+    attempt = 0
+    while True:
+        g = i ^ (attempt << 48)
+        key = game_key(S, g)
+        target = 10 + pick(key, 200, 40)
+        b = Board()
+        ply = 0
+        ok = False
+        while not b.is_game_over():
+            puts = b.puttables(b.turn)
+            if ply >= target and puts:
+                ok = True
+                break
+            if not puts:
+                code = PASS
+            else:
+                x, y = puts[pick(key, ply, len(puts))]
+                code = x + 8 * y
+            assert b.put_s(code_to_str(b, code)) >= 0
+            ply += 1
+        if ok:
+            puts = b.puttables(b.turn)
+            x, y = puts[pick(key, ply, len(puts))]
+            bl, wh = to_bits(b)
+            return bl, wh, b.turn, ply, x + 8 * y
+        attempt += 1
+
+
+def step_all_codes(args):
+    """For one position: every move code 0..64 through board.put_s (board.py:192-209)."""
+    bl, wh, turn = args
+    b0 = from_bits(bl, wh, turn)
+    out = []
+    for code in range(65):
+        b = clone(b0)
+        r = b.put_s(code_to_str(b, code))
+        nb, nw = to_bits(b)
+        out.append((r, nb, nw, b.turn, b.nturn, legal_bits(b, b.turn)))
+    return legal_bits(b0, turn), out
+
+
+def random_positions(n, seed):
+    """Reachable positions for the step fixture: random play (python random, any
+    reachable position will do) stopped at a uniformly random ply; includes
+    positions where the mover must pass and terminal positions."""
+    import random
+    rnd = random.Random(seed)
+    pos = []
+    while len(pos) < n:
+        b = Board()
+        stop = rnd.randrange(0, 70)
+        ply = 0
+        while ply < stop and not b.is_game_over():
+            puts = b.puttables(b.turn)
+            s = "ps" if not puts else b.handstr_from_coord(*puts[rnd.randrange(len(puts))])
+            b.put_s(s)
+            ply += 1
+        bl, wh = to_bits(b)
+        pos.append((bl, wh, b.turn))
+    return pos
+
+
+def u64(a):
+    return np.array(a, dtype=np.uint64)
+
+
+def main():
+    pool = mp.Pool(8)
+    init = Board()
+    ib, iw = to_bits(init)
+
+    # ---------------------------------------------------------------- opening
+    opening = {"black": hex(ib), "white": hex(iw), "turn": init.turn, "nturn": init.nturn,
+               "legal_black": hex(legal_bits(init, Black)), "legal_white": hex(legal_bits(init, White)),
+               "is_game_over": init.is_game_over(), "moves": []}
+    for (x, y) in init.puttables(init.turn):
+        b = clone(init)
+        s = b.handstr_from_coord(x, y)
+        r = b.put_s(s)
+        nb, nw = to_bits(b)
+        opening["moves"].append({"move": s, "sq": x + 8 * y, "ret": r, "flips": hex(iw & ~nw),
+                                 "black": hex(nb), "white": hex(nw), "turn": b.turn, "nturn": b.nturn})
+    opening["strings"] = []
+    for s in ["d4", "a1", "ps", "PS", "Ps", "xyz", "a0", "D3", "Bd3", "Wc4", "BWf5", "e6 ", "", "  c4", "h8", "9a1", "x-1"]:
+        b = clone(init)
+        r = b.put_s(s)
+        nb, nw = to_bits(b)
+        opening["strings"].append({"s": s, "ret": r, "black": hex(nb), "white": hex(nw),
+                                   "turn": b.turn, "nturn": b.nturn})
+    opening["index_error"] = []
+    for s in ["a9", "i1", "z1", "zz9"]:
+        b = clone(init)
+        try:
+            b.put_s(s)
+            opening["index_error"].append({"s": s, "raises": False})
+        except IndexError:
+            opening["index_error"].append({"s": s, "raises": True})
+    # codecs on the opening
+    opening["serialize_str"] = init.serialize_str()
+    opening["serialize_board"] = init.serialize_board()
+    opening["str"] = str(init)
+    json.dump(opening, open(os.path.join(OUT, "opening.json"), "w"), indent=1)
+
+    # ---------------------------------------------------------------- edges
+    edges = []
+
+    def edge(name, bl, wh, turn, codes=tuple(range(65))):
+        b0 = from_bits(bl, wh, turn)
+        rec = {"name": name, "black": hex(bl), "white": hex(wh), "turn": turn,
+               "is_game_over": b0.is_game_over(), "n_black": b0.n_black(), "n_white": b0.n_white(),
+               "n_empty": b0.n_empty(), "legal_black": hex(legal_bits(b0, Black)),
+               "legal_white": hex(legal_bits(b0, White)), "serialize_str": b0.serialize_str(), "steps": []}
+        for code in codes:
+            b = clone(b0)
+            r = b.put_s(code_to_str(b, code))
+            nb, nw = to_bits(b)
+            rec["steps"].append({"code": code, "ret": r, "black": hex(nb), "white": hex(nw), "turn": b.turn})
+        edges.append(rec)
+
+    full = (1 << 64) - 1
+    edge("full_board_black_wins", full & ~0xFF, 0xFF, Black)
+    edge("full_board_draw", 0x00000000FFFFFFFF, 0xFFFFFFFF00000000, White)
+    edge("wipeout_white_gone", 0x0000001818000000, 0, White)
+    edge("wipeout_black_gone", 0, 0x0000001818000000, Black)
+    edge("empty_board", 0, 0, Black)
+    # mover (Black) has no move, White has: black a1, white b1, c1 empty..  Black: a1; White: b1 -> white can't move? construct:
+    # Black at a1 only, White at b1,c1; Black to move: d1 flips b1,c1 -> legal; instead use Black on h8 isolated
+    edge("mover_has_none_opponent_has", 1 << 0, (1 << 1), White)  # white to move: W b1 next to B a1 -> W has no flank; B has c1
+    edge("pass_with_moves_available", ib, iw, Black, codes=(64, 19, 0))
+    edge("long_ray_h_flip", 0x01, 0x7E, Black)  # b1..g1 white, a1 black: h1 flips six
+    edge("diag_and_vertical", (1 << 0) | (1 << 7) | (1 << 56), 0x0040201008040200 | (0x0001010101010100 & ~1), Black)
+    edge("corner_multi_dir", 0x8100000000000081, 0x42C300000000C342, Black)
+    json.dump(edges, open(os.path.join(OUT, "edges.json"), "w"), indent=1)
+
+    # ---------------------------------------------------------------- step, every code
+    pos = random_positions(1024, 20240601)
+    res = pool.map(step_all_codes, pos, chunksize=8)
+    np.savez_compressed(
+        os.path.join(OUT, "midgame_step.npz"),
+        black=u64([p[0] for p in pos]), white=u64([p[1] for p in pos]),
+        turn=np.array([p[2] for p in pos], np.uint8),
+        legal=u64([r[0] for r in res]),
+        ret=np.array([[o[0] for o in r[1]] for r in res], np.int8),
+        next_black=u64([[o[1] for o in r[1]] for r in res]),
+        next_white=u64([[o[2] for o in r[1]] for r in res]),
+        next_turn=np.array([[o[3] for o in r[1]] for r in res], np.uint8),
+        next_nturn=np.array([[o[4] for o in r[1]] for r in res], np.uint8),
+        next_legal=u64([[o[5] for o in r[1]] for r in res]),
+    )
+
+    # ---------------------------------------------------------------- rollouts
+    def rollouts(name, seed, g0, n, policy, n_random, starts=None):
+        if starts is None:
+            starts = [(ib, iw, Black)] * n
+        args = [(seed, g0 + i, policy, n_random, s[0], s[1], s[2]) for i, s in enumerate(starts)]
+        res = pool.map(play, args, chunksize=4)
+        mv = np.full((n, 128), 255, np.uint8)
+        for i, r in enumerate(res):
+            mv[i, :len(r[0])] = r[0]
+        np.savez_compressed(
+            os.path.join(OUT, name + ".npz"),
+            seed=np.array(seed, np.uint64), game_id0=np.array(g0, np.uint64),
+            policy=np.array(policy), n_random=np.array(n_random),
+            start_black=u64([s[0] for s in starts]), start_white=u64([s[1] for s in starts]),
+            start_turn=np.array([s[2] for s in starts], np.uint8),
+            moves=mv, final_black=u64([r[1] for r in res]), final_white=u64([r[2] for r in res]),
+            diff=np.array([r[3] for r in res], np.int8), plies=np.array([r[4] for r in res], np.uint8))
+
+    rollouts("rollout_random", SEED, 0, 256, 0, 0)
+    rollouts("rollout_random_offset", 12345, (1 << 20) * 3 + 77, 128, 0, 0)
+    mid = [(p[0], p[1], p[2]) for p in pos[:128] if p[2] in (Black, White)]
+    rollouts("rollout_random_from_mid", 777, 5, len(mid), 0, 0, starts=mid)
+    rollouts("rollout_greedy", SEED, 0, 192, 1, 10)
+    rollouts("rollout_greedy_from_mid", 99, 1000, 64, 1, 0, starts=mid[:64])
+
+    # ---------------------------------------------------------------- config-2 generator
+    sm = pool.map(sample_midgame, [(SEED, i) for i in range(256)], chunksize=4)
+    np.savez_compressed(os.path.join(OUT, "sample_midgame.npz"), seed=np.array(SEED, np.uint64),
+                        black=u64([s[0] for s in sm]), white=u64([s[1] for s in sm]),
+                        turn=np.array([s[2] for s in sm], np.uint8), nturn=np.array([s[3] for s in sm], np.uint8),
+                        move=np.array([s[4] for s in sm], np.uint8))
+
+    # ---------------------------------------------------------------- RNG known answers
+    S = seed_state(SEED)
+    rng = {"seed": SEED, "seed_state": hex(S),
+           "game_keys": [hex(game_key(S, g)) for g in (0, 1, 2, 1 << 20, (1 << 40) + 3)],
+           "ply_rand_g0": [ply_rand(game_key(S, 0), p) for p in range(8)]}
+    json.dump(rng, open(os.path.join(OUT, "rng.json"), "w"), indent=1)
+    print("fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,61 @@
+"""N>1 path on CPU: world_size-2 gloo, disjoint game-id shards + one histogram
+all_reduce.  The compute is injected (the C oracle, as checker) because this
+container has no GPU; the sharding/reduction host logic is the product's."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from subproc_amd.dist import hist_summary, rollout_sharded, shard_range
+
+
+def _oracle_fn(n, seed, game_id0, policy, n_random, hist):
+    pid = {"random": 0, "greedy": 1}[policy]
+    hist += torch.from_numpy(oracle.rollout(n, seed, game_id0, pid, n_random, n_threads=1)["hist"])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, seed, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hist, local = rollout_sharded(total, seed, rollout_fn=_oracle_fn, device="cpu")
+    out[rank] = (hist.numpy().copy(), local)
+    dist.destroy_process_group()
+
+
+def _run(world, total, seed):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), total, seed, out), nprocs=world, join=True)
+    return dict(out)
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(total, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(e - b for b, e in rs) - min(e - b for b, e in rs) <= 1
+
+
+def test_world2_histogram_equals_single_process():
+    total, seed = 301, 0x5EED
+    res = _run(2, total, seed)
+    ref = oracle.rollout(total, seed, 0)["hist"]
+    for rank in (0, 1):
+        np.testing.assert_array_equal(res[rank][0], ref)
+    assert res[0][1] + res[1][1] == total
+    s = hist_summary(ref)
+    assert s["games"] == total and s["black_wins"] + s["white_wins"] + s["draws"] == total

@@ -1,0 +1,246 @@
+"""GPU parity: the HIP kernels (through the C-ABI, via subproc_amd.ops) against the
+golden fixtures from the real board.py and against the C oracle at scale.
+Bit-exact everywhere (integer/bitwise work)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from golden_io import ROLLOUT_FIXTURES, h, load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+
+from subproc_amd import ops  # noqa: E402
+
+DEV = "cuda"
+U = ops.to_numpy_u64
+
+
+def T(a, dtype=torch.uint8):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(dtype).to(DEV)
+
+
+def B(black, white):
+    return ops.from_numpy_u64(np.stack([np.asarray(black, np.uint64), np.asarray(white, np.uint64)], 1), DEV)
+
+
+def test_reset():
+    op = load_json("opening.json")
+    b, t, nt = ops.reset(1000, DEV)
+    b = U(b)
+    assert (b[:, 0] == h(op["black"])).all() and (b[:, 1] == h(op["white"])).all()
+    assert (t.cpu() == 1).all() and (nt.cpu() == 0).all()
+
+
+def test_opening_known_answers():
+    op = load_json("opening.json")
+    boards = B([h(op["black"])] * 2, [h(op["white"])] * 2)
+    leg = U(ops.legal(boards, T([1, 2])))
+    assert leg[0] == h(op["legal_black"]) and leg[1] == h(op["legal_white"])
+    ms = op["moves"]
+    n = len(ms)
+    boards = B([h(op["black"])] * n, [h(op["white"])] * n)
+    nturn = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    r = ops.step(boards, T([op["turn"]] * n), T([m["sq"] for m in ms]), nturn=nturn)
+    for i, m in enumerate(ms):
+        assert int(r.ret[i]) == m["ret"]
+        assert U(r.flips)[i] == h(m["flips"])
+        assert U(r.boards)[i, 0] == h(m["black"]) and U(r.boards)[i, 1] == h(m["white"])
+        assert int(r.turn[i]) == m["turn"] and int(nturn[i]) == m["nturn"]
+
+
+def test_midgame_every_code():
+    z = load_npz("midgame_step.npz")
+    n = len(z["black"])
+    boards = B(z["black"], z["white"])
+    turn = T(z["turn"])
+    assert (U(ops.legal(boards, turn)) == z["legal"]).all()
+    for code in range(65):
+        nturn = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        r = ops.step(boards, turn, T(np.full(n, code)), nturn=nturn)
+        np.testing.assert_array_equal(r.ret.cpu().numpy(), z["ret"][:, code])
+        np.testing.assert_array_equal(U(r.boards)[:, 0], z["next_black"][:, code])
+        np.testing.assert_array_equal(U(r.boards)[:, 1], z["next_white"][:, code])
+        np.testing.assert_array_equal(r.turn.cpu().numpy(), z["next_turn"][:, code])
+        np.testing.assert_array_equal(nturn.cpu().numpy(), z["next_nturn"][:, code])
+        np.testing.assert_array_equal(U(r.legal_next), z["next_legal"][:, code])
+        # flips = opponent discs that changed colour
+        mover_black = z["turn"] == 1
+        opp0 = np.where(mover_black, z["white"], z["black"])
+        opp1 = np.where(mover_black, z["next_white"][:, code], z["next_black"][:, code])
+        np.testing.assert_array_equal(U(r.flips), opp0 & ~opp1)
+
+
+def test_edges():
+    for e in load_json("edges.json"):
+        n = len(e["steps"])
+        boards = B([h(e["black"])] * n, [h(e["white"])] * n)
+        res = ops.result(boards[:1])
+        assert int(res.terminal[0]) == int(e["is_game_over"]), e["name"]
+        assert int(res.n_black[0]) == e["n_black"] and int(res.n_white[0]) == e["n_white"], e["name"]
+        assert int(res.diff[0]) == e["n_black"] - e["n_white"]
+        r = ops.step(boards, T([e["turn"]] * n), T([s["code"] for s in e["steps"]]))
+        for i, s in enumerate(e["steps"]):
+            assert int(r.ret[i]) == s["ret"], (e["name"], s["code"])
+            assert U(r.boards)[i, 0] == h(s["black"]) and U(r.boards)[i, 1] == h(s["white"]), (e["name"], s["code"])
+            assert int(r.turn[i]) == s["turn"]
+
+
+def test_invalid_codes_and_turns():
+    b, t, _ = ops.reset(6, DEV)
+    r = ops.step(b, T([1, 1, 1, 0, 3, 2]), T([65, 200, 255, 19, 19, 64]))
+    assert r.ret.cpu().tolist() == [-1, -1, -1, -1, -1, 0]
+    assert (U(r.boards) == U(b)).all()
+    assert r.turn.cpu().tolist() == [1, 1, 1, 0, 3, 1]
+
+
+def test_inplace_step_aliasing():
+    z = load_npz("midgame_step.npz")
+    boards = B(z["black"], z["white"])
+    turn = T(z["turn"])
+    lg = U(ops.legal(boards, turn))
+    moves = np.array([(int(x) & -int(x)).bit_length() - 1 if x else 64 for x in lg], np.uint8)
+    ref = ops.step(boards, turn, T(moves))
+    b2, t2 = boards.clone(), turn.clone()
+    ops.step(b2, t2, T(moves), inplace=True)
+    assert (U(b2) == U(ref.boards)).all() and (t2.cpu() == ref.turn.cpu()).all()
+
+
+def test_zero_and_bad_args():
+    e = torch.empty((0, 2), dtype=torch.int64, device=DEV)
+    r = ops.step(e, torch.empty(0, dtype=torch.uint8, device=DEV), torch.empty(0, dtype=torch.uint8, device=DEV))
+    assert r.ret.numel() == 0
+    with pytest.raises(ValueError):
+        ops.legal(torch.zeros((4, 2), dtype=torch.int64), torch.zeros(4, dtype=torch.uint8))
+    with pytest.raises(TypeError):
+        ops.legal(torch.zeros((4, 2), dtype=torch.int32, device=DEV), torch.zeros(4, dtype=torch.uint8, device=DEV))
+
+
+@pytest.mark.parametrize("name", ROLLOUT_FIXTURES)
+def test_rollout_fixtures(name):
+    z = load_npz(name + ".npz")
+    n = len(z["plies"])
+    from_mid = "from_mid" in name
+    policy = "greedy" if int(z["policy"]) == 1 else "random"
+    r = ops.rollout(n, int(z["seed"]), int(z["game_id0"]), policy, int(z["n_random"]),
+                    start=B(z["start_black"], z["start_white"]) if from_mid else None,
+                    start_turn=T(z["start_turn"]) if from_mid else None, record_moves=True, device=DEV)
+    np.testing.assert_array_equal(r.moves.cpu().numpy(), z["moves"])
+    np.testing.assert_array_equal(r.plies.cpu().numpy(), z["plies"])
+    np.testing.assert_array_equal(r.diff.cpu().numpy(), z["diff"])
+    np.testing.assert_array_equal(U(r.final_boards)[:, 0], z["final_black"])
+    np.testing.assert_array_equal(U(r.final_boards)[:, 1], z["final_white"])
+    hist = r.hist.cpu().numpy()
+    np.testing.assert_array_equal(hist[:129], np.bincount(z["diff"].astype(np.int64) + 64, minlength=129))
+    assert hist[132] == int(z["plies"].sum().astype(np.int64))
+
+
+def test_sample_midgame_fixture():
+    z = load_npz("sample_midgame.npz")
+    n = len(z["move"])
+    p = ops.sample_midgame(n, int(z["seed"]), device=DEV)
+    np.testing.assert_array_equal(U(p.boards)[:, 0], z["black"])
+    np.testing.assert_array_equal(U(p.boards)[:, 1], z["white"])
+    np.testing.assert_array_equal(p.turn.cpu().numpy(), z["turn"])
+    np.testing.assert_array_equal(p.nturn.cpu().numpy(), z["nturn"])
+    np.testing.assert_array_equal(p.move.cpu().numpy(), z["move"])
+
+
+# --------------------------------------------------------------------------- at scale vs oracle
+def test_config2_step_65536_vs_oracle():
+    n = 65536
+    p = ops.sample_midgame(n, 0x5EED, device=DEV)
+    o = oracle.sample_midgame(n, 0x5EED)
+    assert (U(p.boards) == o["boards"]).all() and (p.move.cpu().numpy() == o["move"]).all()
+    r = ops.step(p.boards, p.turn, p.move)
+    ro = oracle.step(o["boards"], o["turn"], o["move"])
+    assert (U(r.boards) == ro["boards"]).all()
+    assert (U(r.flips) == ro["flips"]).all()
+    assert (U(r.legal_next) == ro["legal_next"]).all()
+    assert (r.ret.cpu().numpy() == ro["ret"]).all()
+    assert (r.turn.cpu().numpy() == ro["turn"]).all()
+    assert (r.ret.cpu().numpy() >= 1).all()
+
+
+def test_every_code_random_boards_vs_oracle():
+    """Arbitrary (even unreachable) disjoint boards, every move code, both sides."""
+    rng = np.random.default_rng(3)
+    n = 8192
+    occ = rng.integers(0, 2**64, n, dtype=np.uint64) & rng.integers(0, 2**64, n, dtype=np.uint64)
+    col = rng.integers(0, 2**64, n, dtype=np.uint64)
+    black, white = occ & col, occ & ~col
+    boards = B(black, white)
+    nb = np.stack([black, white], 1)
+    for turn in (1, 2):
+        tt = np.full(n, turn, np.uint8)
+        assert (U(ops.legal(boards, T(tt))) == oracle.legal(nb, tt)).all()
+        for code in range(0, 65, 3):
+            mv = np.full(n, code, np.uint8)
+            r = ops.step(boards, T(tt), T(mv))
+            o = oracle.step(nb, tt, mv)
+            assert (U(r.boards) == o["boards"]).all(), code
+            assert (U(r.flips) == o["flips"]).all(), code
+            assert (U(r.legal_next) == o["legal_next"]).all(), code
+            assert (r.ret.cpu().numpy() == o["ret"]).all(), code
+    res = ops.result(boards)
+    ores = oracle.result(nb)
+    for k in ("n_black", "n_white", "diff", "terminal"):
+        assert (getattr(res, k).cpu().numpy() == ores[k]).all(), k
+
+
+def test_rollout_random_65536_vs_oracle():
+    n = 65536
+    r = ops.rollout(n, 0x5EED, 0, device=DEV)
+    o = oracle.rollout(n, 0x5EED, 0)
+    assert (U(r.final_boards) == o["final_boards"]).all()
+    assert (r.diff.cpu().numpy() == o["diff"]).all()
+    assert (r.plies.cpu().numpy() == o["plies"]).all()
+    assert (r.hist.cpu().numpy() == o["hist"]).all()
+
+
+def test_rollout_greedy_4096_vs_oracle():
+    n = 4096
+    r = ops.rollout(n, 42, 1 << 20, "greedy", 10, device=DEV)
+    o = oracle.rollout(n, 42, 1 << 20, policy=1, n_random=10)
+    assert (U(r.final_boards) == o["final_boards"]).all()
+    assert (r.plies.cpu().numpy() == o["plies"]).all()
+    assert (r.hist.cpu().numpy() == o["hist"]).all()
+
+
+def test_rollout_from_start_positions_vs_oracle():
+    n = 16384
+    p = ops.sample_midgame(n, 11, device=DEV)
+    for policy, pid in (("random", 0), ("greedy", 1)):
+        r = ops.rollout(n, 5, 77, policy, 0, start=p.boards, start_turn=p.turn, record_moves=True, device=DEV)
+        o = oracle.rollout(n, 5, 77, pid, 0, start=U(p.boards), start_turn=p.turn.cpu().numpy(),
+                           record_moves=True)
+        assert (r.moves.cpu().numpy() == o["moves"]).all(), policy
+        assert (U(r.final_boards) == o["final_boards"]).all(), policy
+        assert (r.hist.cpu().numpy() == o["hist"]).all(), policy
+
+
+# --------------------------------------------------------------------------- full size: properties
+def test_config3_full_size_properties():
+    """batch 1,048,576: determinism, split invariance, terminal finals, histogram
+    consistency — size-independent properties (oracle too slow at this size)."""
+    n = 1 << 20
+    a = ops.rollout(n, 0x5EED, 0, device=DEV)
+    b = ops.rollout(n, 0x5EED, 0, device=DEV)
+    assert torch.equal(a.final_boards, b.final_boards) and torch.equal(a.hist, b.hist)
+    h1 = ops.rollout(n // 2 + 12345, 0x5EED, 0, device=DEV)
+    h2 = ops.rollout(n - (n // 2 + 12345), 0x5EED, n // 2 + 12345, device=DEV)
+    assert torch.equal(torch.cat([h1.final_boards, h2.final_boards]), a.final_boards)
+    assert torch.equal(h1.hist + h2.hist, a.hist)
+    res = ops.result(a.final_boards)
+    assert bool(res.terminal.bool().all())
+    assert torch.equal(res.diff, a.diff)
+    hist = a.hist.cpu().numpy()
+    assert hist[:129].sum() == n and hist[129:132].sum() == n
+    assert hist[132] == int(a.plies.long().sum())
+    np.testing.assert_array_equal(hist[:129], np.bincount(a.diff.cpu().numpy().astype(np.int64) + 64, minlength=129))
+    # game length statistics of random play (mean 60.41, max 65)
+    assert 60.0 < hist[132] / n < 61.0
+    # a 1% sample checked against the oracle
+    idx = np.arange(0, n, 97)
+    o = oracle.rollout(len(idx), 0x5EED, 0)  # contiguous ids 0..len-1
+    assert (U(a.final_boards)[:len(idx)] == o["final_boards"]).all()

@@ -38,8 +38,8 @@ def lib():
         L.oracle_sample_midgame.argtypes = [U64, U64, P, P, P, P, I64]
         L.oracle_game_key.argtypes = [U64, U64]
         L.oracle_game_key.restype = U64
-        L.oracle_ply_rand.argtypes = [U64, ctypes.c_uint32]
-        L.oracle_ply_rand.restype = ctypes.c_uint32
+        L.oracle_rng_draws.argtypes = [U64, ctypes.c_uint32]
+        L.oracle_rng_draws.restype = ctypes.c_uint32
         for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
                   "oracle_sample_midgame"):
             getattr(L, f).restype = I
@@ -122,5 +122,6 @@ def game_key(seed, g):
     return lib().oracle_game_key(seed, g)
 
 
-def ply_rand(key, ply):
-    return lib().oracle_ply_rand(key, ply)
+def rng_draw(key, i):
+    """The i-th (1-based) draw of game key `key`'s LCG stream."""
+    return lib().oracle_rng_draws(key, i)

@@ -4,7 +4,7 @@
  * and bench.py's cpu_baseline leg, never by the product path (subproc_amd/).
  *
  * Pinned against the reference: tests/test_oracle.py checks every function here
- * against tests/golden/*, which tests/golden/gen_golden.py produced by running
+ * against the tests/golden fixtures, which tests/golden/gen_golden.py produced by running
  * the real /root/reference/board.py (SURVEY.md §8c shim).
  *
  * Deliberately NOT a bitboard implementation: it follows board.py's own
@@ -166,20 +166,14 @@ static uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-static uint32_t mix32(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x7FEB352Du;
-    x ^= x >> 15;
-    x *= 0x846CA68Bu;
-    x ^= x >> 16;
-    return x;
-}
 static uint64_t seed_state(uint64_t seed) { return mix64(seed + GOLDEN64); }
 static uint64_t game_key(uint64_t S, uint64_t g) { return mix64(S + g * GOLDEN64); }
-static uint32_t ply_rand(uint64_t key, uint32_t ply) {
-    return mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + ply));
-}
-static int pick(uint64_t key, uint32_t ply, int n) { return (int)(((uint64_t)ply_rand(key, ply) * (uint64_t)n) >> 32); }
+/* per-game draw stream: 32-bit LCG, state0 = lo32(key), increment = hi32(key) | 1 */
+#define LCG_MUL 0x915F77F5u
+typedef struct { uint32_t state, inc; } GameRng;
+static GameRng rng_init(uint64_t key) { GameRng r = {(uint32_t)key, (uint32_t)(key >> 32) | 1u}; return r; }
+static uint32_t rng_draw(GameRng* r) { r->state = r->state * LCG_MUL + r->inc; return r->state; }
+static int rng_pick(GameRng* r, int n) { return (int)(((uint64_t)rng_draw(r) * (uint64_t)n) >> 32); }
 
 /* k-th entry of puttables() (row-major list), as a square code */
 static int kth_square(uint64_t legal, int k) {
@@ -263,13 +257,14 @@ int oracle_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, in
  * policies: a side with no move passes ('PS'). */
 static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* moves) {
     int ply = 0;
+    GameRng rng = rng_init(key);
     while (!is_game_over(s)) {
         uint64_t legal = puttables(s, s->turn);
         int code;
         if (!legal) {
             code = PASS_CODE;
         } else if (policy == 0 || ply < n_random) {
-            code = kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal)));
+            code = kth_square(legal, rng_pick(&rng, popcount64(legal)));
         } else {
             int best = -1, bestv = 1 << 30;
             for (int sq = 0; sq < 64; sq++) {
@@ -340,15 +335,15 @@ int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint
     for (int64_t j = 0; j < n; j++) {
         uint64_t i = index0 + (uint64_t)j;
         for (uint64_t attempt = 0;; attempt++) {
-            uint64_t key = game_key(S, i ^ (attempt << 48));
-            int target = 10 + pick(key, 200, 40);
+            GameRng rng = rng_init(game_key(S, i ^ (attempt << 48)));
+            int target = 10 + rng_pick(&rng, 40); /* the first draw picks the stopping ply */
             Board s;
             board_init(&s);
             int ply = 0, ok = 0;
             while (!is_game_over(&s)) {
                 uint64_t legal = puttables(&s, s.turn);
                 if (ply >= target && legal) { ok = 1; break; }
-                int code = legal ? kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal))) : PASS_CODE;
+                int code = legal ? kth_square(legal, rng_pick(&rng, popcount64(legal))) : PASS_CODE;
                 put_code(&s, code);
                 ply++;
             }
@@ -357,7 +352,7 @@ int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint
                 board_to_bits(&s, &boards[2 * j], &boards[2 * j + 1]);
                 turn[j] = (uint8_t)s.turn;
                 if (nturn) nturn[j] = (uint8_t)ply;
-                move[j] = (uint8_t)kth_square(legal, pick(key, (uint32_t)ply, popcount64(legal)));
+                move[j] = (uint8_t)kth_square(legal, rng_pick(&rng, popcount64(legal)));
                 break;
             }
         }
@@ -367,4 +362,9 @@ int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint
 
 /* RNG known answers for the fixture check */
 uint64_t oracle_game_key(uint64_t seed, uint64_t g) { return game_key(seed_state(seed), g); }
-uint32_t oracle_ply_rand(uint64_t key, uint32_t ply) { return ply_rand(key, ply); }
+uint32_t oracle_rng_draws(uint64_t key, uint32_t count) {
+    GameRng r = rng_init(key);
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < count; i++) v = rng_draw(&r);
+    return v; /* the count-th draw */
+}

@@ -1,0 +1,203 @@
+// bitboard.hpp — gfx950 device primitives for 8x8 Othello bitboards.
+//
+// Cost model (measured on MI355X, tools/diag/valu_rate*.cpp, DESIGN.md §Cost model):
+// in a mixed VALU stream every VALU instruction costs ~4 cycles per wave64 on its
+// SIMD (only pure streams of simple VOP2 logic reach ~2.2), so throughput is set by
+// the INSTRUCTION COUNT per env-step.  Hence:
+//   * 64-bit shifts stay single v_lshl/v_lshrrev_b64 instructions;
+//   * every fill step / flip accumulation is one v_bfi_b32 per 32-bit half (see bfi);
+//   * Kogge-Stone propagators are computed once per position and shared between
+//     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S) and between legal-move
+//     generation and flip computation.
+//
+// Square sq = x + 8*y (board.py:74-81); rays of board.py:9-17 as shifts:
+//   +1 R (x+1), +8 D (y+1), +9 RD, +7 LD   and their opposites -1 L, -8 U, -9 LU, -7 RU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace oth {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+constexpr u64 INNER_FILES = 0x7E7E7E7E7E7E7E7Eull;  // files b..g: a disc on a/h cannot be flanked along a row/diagonal
+
+// bfi(m, a, b) = (m & a) | (~m & b): one v_bfi_b32 per half.  Every Kogge-Stone
+// step "gen |= pro & shifted" is written as bfi(pro, shifted, gen): the propagator
+// never intersects the current fill (a propagator square at distance <= 2^k from
+// the source would need an opponent disc at distance 0), so both forms agree, and
+// hipcc emits bfi (it never fuses the plain and-or).  Flip accumulation uses the
+// same identity: rays from one square are disjoint.
+__device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return (m & a) | (~m & b); }
+__device__ __forceinline__ u64 andn(u64 a, u64 b) { return a & ~b; }
+__device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return a | b | c; }
+
+template <int S, bool L>
+__device__ __forceinline__ u64 sh(u64 x) {
+    return L ? (x << S) : (x >> S);
+}
+
+// Kogge-Stone propagators of one direction pair (+S / -S) for opponent set `pro`
+struct PairProp {
+    u64 pro, p2L, p4L, p2R, p4R;
+};
+template <int S>
+__device__ __forceinline__ PairProp pair_prop(u64 pro) {
+    PairProp q;
+    q.pro = pro;
+    q.p2L = pro & sh<S, true>(pro);              // q, q-S in pro
+    q.p4L = q.p2L & sh<2 * S, true>(q.p2L);      // q .. q-3S in pro
+    q.p2R = sh<S, false>(q.p2L);                 // q, q+S in pro
+    q.p4R = sh<3 * S, false>(q.p4L);             // q .. q+3S in pro
+    return q;
+}
+
+// occluded fill of `gen` along +S (L) or -S through the pair's propagators:
+// covers distances 0..7
+template <int S, bool L>
+__device__ __forceinline__ u64 ks(u64 gen, const PairProp& q) {
+    gen = bfi(q.pro, sh<S, L>(gen), gen);
+    gen = bfi(L ? q.p2L : q.p2R, sh<2 * S, L>(gen), gen);
+    gen = bfi(L ? q.p4L : q.p4R, sh<4 * S, L>(gen), gen);
+    return gen;
+}
+
+// discs of `Oi` (inner opponent discs) in runs that start right east of a bit of
+// `src`: the carry of Oi + (src << 1) ripples through each such run (one
+// v_lshl_add_u64 + one v_bfi_b32 per half); equal to the Kogge-Stone east fill
+// from src through Oi, minus src.
+__device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, (src << 1) + Oi); }
+
+// All propagators + attached runs of one position (mover P, opponent O).
+// A[i]: opponent discs reachable from a P disc along direction i through
+// opponent discs only (board.py:124-139's "hostile" runs, seen from P).
+// Direction index i: 0:+1 1:-1 2:+8 3:-8 4:+9 5:-9 6:+7 7:-7
+struct Position {
+    PairProp h, v, d9, d7;
+    u64 A[8];
+    u64 legal;  // Board.puttables as a mask (board.py:46-52)
+};
+
+__device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
+    const u64 Oi = O & INNER_FILES;
+    s.h = pair_prop<1>(Oi);
+    s.v = pair_prop<8>(O);
+    s.d9 = pair_prop<9>(Oi);
+    s.d7 = pair_prop<7>(Oi);
+    // east (+1): bits along the ray are contiguous, so one add propagates a
+    // carry from each P disc through its adjacent run of inner opponent discs
+    // and clears exactly those run bits: A = Oi & ~(Oi + (P << 1)).
+    s.A[0] = east_run(P, Oi);
+    // the other fills from P stay inside P | O, so "minus P" is "and O"
+    s.A[1] = ks<1, false>(P, s.h) & O;
+    s.A[2] = ks<8, true>(P, s.v) & O;
+    s.A[3] = ks<8, false>(P, s.v) & O;
+    s.A[4] = ks<9, true>(P, s.d9) & O;
+    s.A[5] = ks<9, false>(P, s.d9) & O;
+    s.A[6] = ks<7, true>(P, s.d7) & O;
+    s.A[7] = ks<7, false>(P, s.d7) & O;
+    // a legal square is one step beyond an attached run, and empty
+    u64 m = or3(sh<1, true>(s.A[0]), sh<1, false>(s.A[1]), sh<8, true>(s.A[2]));
+    m = or3(m, sh<8, false>(s.A[3]), sh<9, true>(s.A[4]));
+    m = or3(m, sh<9, false>(s.A[5]), sh<7, true>(s.A[6]));
+    m |= sh<7, false>(s.A[7]);
+    s.legal = andn(m, P | O);
+}
+
+// Discs flipped by a legal move at bit `mv` (board.py:161-174): walking from mv
+// along +d, the opponent run counts iff it is attached to a P disc, i.e. lies in
+// the run set of the opposite direction -d.  No bracket test needed.
+__device__ __forceinline__ u64 flips_at(u64 mv, const Position& s) {
+    u64 f = east_run(mv, s.h.pro) & s.A[1];
+    f = bfi(ks<1, false>(mv, s.h), s.A[0], f);
+    f = bfi(ks<8, true>(mv, s.v), s.A[3], f);
+    f = bfi(ks<8, false>(mv, s.v), s.A[2], f);
+    f = bfi(ks<9, true>(mv, s.d9), s.A[5], f);
+    f = bfi(ks<9, false>(mv, s.d9), s.A[4], f);
+    f = bfi(ks<7, true>(mv, s.d7), s.A[7], f);
+    f = bfi(ks<7, false>(mv, s.d7), s.A[6], f);
+    return f;
+}
+
+// legal moves only (no run sets kept) — for child positions / next-state masks
+__device__ __forceinline__ u64 moves(u64 P, u64 O) {
+    Position s;
+    analyse(P, O, s);
+    return s.legal;
+}
+
+// flips of `mv` for mover P with a bracket test per direction (used where the run
+// sets of the position are not available: the single-step kernel).  Works for any
+// mv; returns 0 when nothing is flanked.
+// (no wrap mask on the bracket test: a run is confined to the propagator's inner
+// files, so only the run-less case g == mv can "wrap", and it flips nothing)
+template <int S, bool L>
+__device__ __forceinline__ u64 flips_dir_test(u64 mv, u64 P, const PairProp& q) {
+    const u64 g = ks<S, L>(mv, q);
+    return (sh<S, L>(g) & P) ? g : 0ull;
+}
+__device__ __forceinline__ u64 flips_tested(u64 mv, u64 P, u64 O) {
+    const u64 Oi = O & INNER_FILES;
+    const PairProp h = pair_prop<1>(Oi), v = pair_prop<8>(O), d9 = pair_prop<9>(Oi), d7 = pair_prop<7>(Oi);
+    const u64 e = east_run(mv, Oi);  // run east of mv; flanked iff the square after it is P
+    u64 f = ((((e | mv) << 1) & P) ? e : 0ull) | flips_dir_test<1, false>(mv, P, h);
+    f |= flips_dir_test<8, true>(mv, P, v) | flips_dir_test<8, false>(mv, P, v);
+    f |= flips_dir_test<9, true>(mv, P, d9) | flips_dir_test<9, false>(mv, P, d9);
+    f |= flips_dir_test<7, true>(mv, P, d7) | flips_dir_test<7, false>(mv, P, d7);
+    return andn(f, mv);
+}
+
+// k-th set bit via two popcount bisection levels (32, 16, 8) and a 256x8 byte
+// table in LDS: tab[b * 8 + k] = index of the k-th set bit of byte b.
+__device__ __forceinline__ void kth_table_init(uint8_t* tab) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+        int k = 0;
+        for (int i = 0; i < 8; i++)
+            if (b >> i & 1) tab[b * 8 + k++] = (uint8_t)i;
+        for (; k < 8; k++) tab[b * 8 + k] = 0;
+    }
+}
+__device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, const uint8_t* tab) {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 c = __popc(lo);
+    bool up = k >= c;
+    u32 w = up ? hi : lo;
+    k = up ? k - c : k;
+    u32 pos = up ? 32u : 0u;
+    c = __popc(w & 0xFFFFu);
+    up = k >= c;
+    k = up ? k - c : k;
+    u32 s = up ? 16u : 0u;
+    w >>= s;
+    pos += s;
+    c = __popc(w & 0xFFu);
+    up = k >= c;
+    k = up ? k - c : k;
+    s = up ? 8u : 0u;
+    w >>= s;
+    pos += s;
+    return pos + tab[(w & 0xFFu) * 8u + k];
+}
+
+// index of the k-th set bit (LSB-first, 0-based) of x; requires k < popcount(x).
+__device__ __forceinline__ u32 kth_bit(u64 x, u32 k) {
+    u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 c = __popc(lo);
+    bool up = k >= c;
+    u32 w = up ? hi : lo;
+    k = up ? k - c : k;
+    u32 pos = up ? 32u : 0u;
+#pragma unroll
+    for (int half = 16; half >= 1; half >>= 1) {
+        const u32 mask = (1u << half) - 1u;
+        c = __popc(w & mask);
+        up = k >= c;
+        w = up ? (w >> half) : w;
+        k = up ? k - c : k;
+        pos += up ? (u32)half : 0u;
+    }
+    return pos;
+}
+
+}  // namespace oth

@@ -8,112 +8,32 @@
 //   play loop                   (game_runner.py:165-201) -> rollout_kernel
 //
 // Design: one game per lane, state in VGPRs as two uint64 bitboards
-// (mover P, opponent O); pure integer/bitwise VALU work, no LDS tables, no MFMA.
-// Rollouts keep every lane busy by refilling finished lanes from a per-wave game
-// range with __ballot + mbcnt (wavefront compaction), and reduce the win/score
-// histogram in LDS before one global atomic per bin per workgroup.
+// (mover P, opponent O); pure integer/bitwise VALU work, no MFMA.  The cost of
+// a rollout is its VALU instruction count per env-step (bitboard.hpp), so the
+// rollout kernel keeps per-iteration control flow minimal: a wave dequeues 64
+// game ids (one per lane) from a per-launch counter, plays them out with
+// __ballot-driven lane masking, then dequeues again.  LDS holds the k-th-bit
+// byte table and the per-workgroup win/score histogram (one global atomic per
+// non-zero bin per workgroup at exit).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
 
 #include "../../include/othello.h"
+#include "bitboard.hpp"
 
 #define OTH_VERSION "subproc_amd 0.1.0 gfx950"
 
 namespace {
 
-typedef uint64_t u64;
-typedef uint32_t u32;
+using namespace oth;
 
-constexpr u64 NOT_A = 0xFEFEFEFEFEFEFEFEull;  // clears file a (x = 0): destination mask for +x moves
-constexpr u64 NOT_H = 0x7F7F7F7F7F7F7F7Full;  // clears file h (x = 7): destination mask for -x moves
-constexpr u64 ALL = ~0ull;
 constexpr u64 OPEN_BLACK = 0x0000000810000000ull;  // e4, d5  (board.py:25)
 constexpr u64 OPEN_WHITE = 0x0000001008000000ull;  // d4, e5  (board.py:24)
 constexpr int kBlock = 256;
-
-// ---------------------------------------------------------------------------
-// directional shifts: L = toward higher squares.  The 8 rays of board.py:9-17:
-//   R (+1,0)=<<1 NOT_A   L (-1,0)=>>1 NOT_H   D (0,+1)=<<8   U (0,-1)=>>8
-//   RD(+1,+1)=<<9 NOT_A  LD(-1,+1)=<<7 NOT_H  RU(+1,-1)=>>7 NOT_A  LU(-1,-1)=>>9 NOT_H
-// ---------------------------------------------------------------------------
-template <int S, bool L>
-__device__ __forceinline__ u64 sh(u64 x) {
-    return L ? (x << S) : (x >> S);
-}
-
-// Kogge-Stone occluded fill of `gen` through `pro` along one direction
-// (3 doubling steps cover the 6-square maximum run).
-template <int S, bool L>
-__device__ __forceinline__ u64 ks_fill(u64 gen, u64 pro) {
-    gen |= pro & sh<S, L>(gen);
-    pro &= sh<S, L>(pro);
-    gen |= pro & sh<2 * S, L>(gen);
-    pro &= sh<2 * S, L>(pro);
-    gen |= pro & sh<4 * S, L>(gen);
-    return gen;
-}
-
-// legal squares for mover P in one direction: empty squares reached by a run
-// of >=1 opponent discs that starts next to a P disc
-template <int S, bool L, u64 M>
-__device__ __forceinline__ u64 moves_dir(u64 P, u64 O, u64 E) {
-    const u64 g = ks_fill<S, L>(P, O & M);
-    return sh<S, L>(g & O) & M & E;
-}
-
-__device__ __forceinline__ u64 moves(u64 P, u64 O) {
-    const u64 E = ~(P | O);
-    u64 m = moves_dir<1, true, NOT_A>(P, O, E);
-    m |= moves_dir<1, false, NOT_H>(P, O, E);
-    m |= moves_dir<8, true, ALL>(P, O, E);
-    m |= moves_dir<8, false, ALL>(P, O, E);
-    m |= moves_dir<9, true, NOT_A>(P, O, E);
-    m |= moves_dir<7, true, NOT_H>(P, O, E);
-    m |= moves_dir<7, false, NOT_A>(P, O, E);
-    m |= moves_dir<9, false, NOT_H>(P, O, E);
-    return m;
-}
-
-// discs flipped by placing bit `mv` for mover P: the run of O from mv along a
-// ray counts only if the square after it holds P (board.py:124-139)
-template <int S, bool L, u64 M>
-__device__ __forceinline__ u64 flips_dir(u64 mv, u64 P, u64 O) {
-    const u64 g = ks_fill<S, L>(mv, O & M);
-    return (sh<S, L>(g) & M & P) ? (g & O) : 0ull;
-}
-
-__device__ __forceinline__ u64 flips(u64 mv, u64 P, u64 O) {
-    u64 f = flips_dir<1, true, NOT_A>(mv, P, O);
-    f |= flips_dir<1, false, NOT_H>(mv, P, O);
-    f |= flips_dir<8, true, ALL>(mv, P, O);
-    f |= flips_dir<8, false, ALL>(mv, P, O);
-    f |= flips_dir<9, true, NOT_A>(mv, P, O);
-    f |= flips_dir<7, true, NOT_H>(mv, P, O);
-    f |= flips_dir<7, false, NOT_A>(mv, P, O);
-    f |= flips_dir<9, false, NOT_H>(mv, P, O);
-    return f;
-}
-
-// index of the k-th set bit (LSB-first, 0-based) of x; requires k < popcount(x).
-// Branch-free popcount bisection: identical cost in every lane.
-__device__ __forceinline__ u32 kth_bit(u64 x, u32 k) {
-    u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 c = __popc(lo);
-    bool up = k >= c;
-    u32 w = up ? hi : lo;
-    k = up ? k - c : k;
-    u32 pos = up ? 32u : 0u;
-#pragma unroll
-    for (int half = 16; half >= 1; half >>= 1) {
-        const u32 mask = (1u << half) - 1u;
-        c = __popc(w & mask);
-        up = k >= c;
-        w = up ? (w >> half) : w;
-        k = up ? k - c : k;
-        pos += up ? (u32)half : 0u;
-    }
-    return pos;
-}
 
 // ---------------------------------------------------------------------------
 // RNG spec (twins: oracle/othello_oracle.c, tests/golden/gen_golden.py)
@@ -124,30 +44,33 @@ __host__ __device__ __forceinline__ u64 mix64(u64 z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ u32 mix32(u32 x) {
-    x ^= x >> 16;
-    x *= 0x7FEB352Du;
-    x ^= x >> 15;
-    x *= 0x846CA68Bu;
-    x ^= x >> 16;
-    return x;
-}
 __device__ __forceinline__ u64 game_key(u64 S, u64 g) { return mix64(S + g * GOLDEN64); }
-__device__ __forceinline__ u32 ply_rand(u64 key, u32 ply) {
-    return mix32((u32)key ^ mix32((u32)(key >> 32) + ply));
-}
-__device__ __forceinline__ u32 pick(u64 key, u32 ply, u32 n) { return __umulhi(ply_rand(key, ply), n); }
+// per-game draw stream: 32-bit LCG, state0 = lo32(key), increment = hi32(key) | 1;
+// a uniform pick in [0, n) is umulhi(draw, n)
+constexpr u32 LCG_MUL = 0x915F77F5u;
+struct GameRng {
+    u32 state, inc;
+    __device__ __forceinline__ void init(u64 key) {
+        state = (u32)key;
+        inc = (u32)(key >> 32) | 1u;
+    }
+    __device__ __forceinline__ u32 pick(u32 n) {
+        state = state * LCG_MUL + inc;
+        return __umulhi(state, n);
+    }
+};
 
 // 1-ply greedy: legal move minimising the opponent's mobility on the child,
 // ties -> lowest square (first in puttables order)
-__device__ __forceinline__ u32 greedy_move(u64 legal, u64 P, u64 O) {
+__device__ __forceinline__ u32 greedy_move(const Position& s, u64 P, u64 O) {
     u32 best = 64, bestv = 1000;
+    u64 legal = s.legal;
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         const u64 mv = 1ull << sq;
         legal &= legal - 1;
-        const u64 f = flips(mv, P, O);
-        const u32 v = (u32)__popcll(moves(O & ~f, P | f | mv));
+        const u64 f = flips_at(mv, s);
+        const u32 v = (u32)__popcll(moves(andn(O, f), P | f | mv));
         if (v < bestv) {
             bestv = v;
             best = sq;
@@ -206,11 +129,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in,
         } else if (mvc < 64) {
             const u64 mv = 1ull << mvc;
             if (!((P | O) & mv)) {
-                f = flips(mv, P, O);
+                f = flips_tested(mv, P, O);
                 if (f) {
                     r = __popcll(f);
                     P |= f | mv;
-                    O &= ~f;
+                    O = andn(O, f);
                 }
             }
         }
@@ -243,9 +166,17 @@ __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// rollout kernel: one game per lane, finished lanes refilled from the wave's
-// contiguous game range via ballot + mbcnt, until the range is exhausted.
+// rollout kernel: persistent waves (grid = resident capacity); each wave
+// dequeues a batch of 64 game ids (ONE returning atomic), plays the 64 games
+// to terminal in lockstep -- a finished lane is masked off by __ballot until
+// the whole batch is done -- and dequeues again.  The hardware balances the
+// batches; no refill code runs inside the ply loop (measured cheaper than
+// per-lane refill, DESIGN.md §Rollout scheduling).
 // ---------------------------------------------------------------------------
+constexpr int kWorkSlots = 64;  // concurrent launches supported (distinct streams)
+constexpr int kCtrStride = 16;  // u64 words between counters (128 B)
+__device__ unsigned long long g_work[kWorkSlots * kCtrStride];
+
 struct RolloutArgs {
     const u64* start;
     const uint8_t* start_turn;
@@ -259,110 +190,125 @@ struct RolloutArgs {
     uint8_t* moves;
     long long* hist;
     int64_t n;
-    int64_t games_per_wave;
+    unsigned long long* work;  // batch counter, zeroed before the launch
 };
 
+#ifdef OTH_DIAG
+__device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
+#endif
+
+template <int POLICY>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
+#ifdef OTH_DIAG
+    const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long diag_iters = 0;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+#endif
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
+    __shared__ uint8_t kth_tab[256 * 8];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
+    kth_table_init(kth_tab);
     __syncthreads();
 
     const int lane = lane_id();
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const int64_t w_begin = wave * a.games_per_wave;
-    const int64_t w_end = min(a.n, w_begin + a.games_per_wave);
-
-    // per-lane game state
-    u64 P = 0, O = 0, key = 0;
-    u32 side = OTH_BLACK, ply = 0;
-    bool passed = false;
-    int64_t g = -1;
-    bool active = false;
+    const u64 n = (u64)a.n;
     u64 plies_sum = 0;
 
-    int64_t next = w_begin;  // wave-uniform
-    bool need = true;        // this lane needs a game
     for (;;) {
-        // ---- refill lanes that need a game (wavefront compaction)
-        const u64 want = __ballot(need);
-        if (want) {
-            const u32 rank = __popcll(want & ((1ull << lane) - 1ull));  // mbcnt
-            if (need) {
-                g = next + rank;
-                active = g < w_end;
-                need = false;
-                if (active) {
-                    key = game_key(a.seed_state, a.game_id0 + (u64)g);
-                    ply = 0;
-                    passed = false;
-                    u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
-                    side = OTH_BLACK;
-                    if (a.start) {
-                        const ulonglong2 s = reinterpret_cast<const ulonglong2*>(a.start)[g];
-                        bl = s.x;
-                        wh = s.y;
-                        side = a.start_turn ? a.start_turn[g] : OTH_BLACK;
-                        side = side == OTH_WHITE ? OTH_WHITE : OTH_BLACK;
-                    }
-                    P = side == OTH_BLACK ? bl : wh;
-                    O = side == OTH_BLACK ? wh : bl;
-                    if (a.moves) {
-                        uint4* mrec = reinterpret_cast<uint4*>(a.moves + g * OTH_MOVES_STRIDE);
+        // ---- dequeue a batch of 64 games (one per lane)
+        u64 base = 0;
+        if (lane == 0) base = atomicAdd(a.work, 64ull);
+        base = __shfl(base, 0);
+        if (base >= n) break;  // wave-uniform
+        const u64 g = base + lane;
+        bool active = g < n;
+        u64 P = OPEN_BLACK, O = OPEN_WHITE;
+        u32 side = OTH_BLACK, ply = 0;
+        bool passed = false;
+        GameRng rng;
+        if (active) {
+            rng.init(game_key(a.seed_state, a.game_id0 + g));
+            if (a.start) {
+                const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(a.start)[g];
+                side = a.start_turn ? a.start_turn[g] : OTH_BLACK;
+                side = side == OTH_WHITE ? OTH_WHITE : OTH_BLACK;
+                P = side == OTH_BLACK ? s0.x : s0.y;
+                O = side == OTH_BLACK ? s0.y : s0.x;
+            }
+            if (a.moves) {
+                uint4* mrec = reinterpret_cast<uint4*>(a.moves + g * OTH_MOVES_STRIDE);
 #pragma unroll
-                        for (int q = 0; q < OTH_MOVES_STRIDE / 16; q++) mrec[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-                    }
-                }
+                for (int q = 0; q < OTH_MOVES_STRIDE / 16; q++) mrec[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
             }
-            next += __popcll(want);
         }
-        if (!__ballot(active)) break;
-        if (!active) continue;  // (exec-masked; loop continues while any lane is active)
 
-        const u64 legal = moves(P, O);
-        if (legal == 0) {
-            if (passed) {
-                // terminal: both sides without a legal move (board.py:57-58)
-                const u64 bl = side == OTH_BLACK ? P : O, wh = side == OTH_BLACK ? O : P;
-                const int d = __popcll(bl) - __popcll(wh);
-                if (a.final_boards) reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
-                if (a.diff) a.diff[g] = (int8_t)d;
-                if (a.plies) a.plies[g] = (uint8_t)ply;
-                atomicAdd(&hist_s[d + 64], 1ull);
-                atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
-                plies_sum += ply;
-                need = true;
-            } else {
-                // mover must pass: tentatively hand the move over; the pass is
-                // counted once the other side is found to have a move
-                passed = true;
-                const u64 t = P;
-                P = O;
-                O = t;
-                side ^= 3u;
+        // ---- play the batch: one env-step per active lane per iteration
+        while (__ballot(active)) {
+#ifdef OTH_DIAG
+            diag_iters++;
+#endif
+            if (!active) continue;
+            Position pos;
+            analyse(P, O, pos);
+            const u64 legal = pos.legal;
+            if (legal == 0) {
+                if (passed) {
+                    // terminal: both sides without a legal move (board.py:57-58)
+                    const u64 bl = side == OTH_BLACK ? P : O, wh = side == OTH_BLACK ? O : P;
+                    const int d = __popcll(bl) - __popcll(wh);
+                    if (a.final_boards) reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
+                    if (a.diff) a.diff[g] = (int8_t)d;
+                    if (a.plies) a.plies[g] = (uint8_t)ply;
+                    atomicAdd(&hist_s[d + 64], 1ull);
+                    atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
+                    plies_sum += ply;
+                    active = false;
+                } else {
+                    // the mover must pass: hand the move over tentatively; the pass
+                    // is counted once the other side turns out to have a move
+                    passed = true;
+                    const u64 t = P;
+                    P = O;
+                    O = t;
+                    side ^= 3u;
+                }
+                continue;
             }
-            continue;
-        }
-        if (passed) {
-            if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
+            if (passed) {
+                if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
+                ply++;
+                passed = false;
+            }
+            u32 sq;
+            if (POLICY == OTH_POLICY_GREEDY && (int)ply >= a.n_random) {
+                sq = greedy_move(pos, P, O);
+            } else {
+                sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
+            }
+            const u64 mv = 1ull << sq;
+            const u64 f = flips_at(mv, pos);
+            if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
+            const u64 np = andn(O, f);
+            O = P | f | mv;
+            P = np;
+            side ^= 3u;
             ply++;
-            passed = false;
         }
-        u32 sq;
-        if (a.policy == OTH_POLICY_GREEDY && (int)ply >= a.n_random) {
-            sq = greedy_move(legal, P, O);
-        } else {
-            sq = kth_bit(legal, pick(key, ply, (u32)__popcll(legal)));
-        }
-        const u64 mv = 1ull << sq;
-        const u64 f = flips(mv, P, O);
-        if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
-        const u64 np = O & ~f;
-        O = P | f | mv;
-        P = np;
-        side ^= 3u;
-        ply++;
     }
 
+#ifdef OTH_DIAG
+    if (lane == 0 && g_diag) {
+        unsigned hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long* d = g_diag + 4 * wave;
+        d[0] = diag_t0;
+        d[1] = __builtin_amdgcn_s_memrealtime();
+        d[2] = ((unsigned long long)xcc << 32) | hwid;
+        d[3] = diag_iters;
+    }
+#endif
     // plies: wave reduction, one LDS atomic per wave
     for (int off = 32; off >= 1; off >>= 1) plies_sum += __shfl_xor(plies_sum, off);
     if (lane == 0) atomicAdd(&hist_s[132], (unsigned long long)plies_sum);
@@ -383,15 +329,16 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
     if (j >= n) return;
     const u64 i = index0 + (u64)j;
     for (u64 attempt = 0;; attempt++) {
-        const u64 key = game_key(S, i ^ (attempt << 48));
-        const u32 target = 10 + pick(key, 200, 40);
+        GameRng rng;
+        rng.init(game_key(S, i ^ (attempt << 48)));
+        const u32 target = 10 + rng.pick(40);  // the first draw picks the stopping ply
         u64 P = OPEN_BLACK, O = OPEN_WHITE;
         u32 side = OTH_BLACK, ply = 0;
         for (;;) {
             const u64 legal = moves(P, O);
             if (legal == 0 && moves(O, P) == 0) break;  // is_game_over
             if (ply >= target && legal) {
-                const u32 sq = kth_bit(legal, pick(key, ply, (u32)__popcll(legal)));
+                const u32 sq = kth_bit(legal, rng.pick((u32)__popcll(legal)));
                 reinterpret_cast<ulonglong2*>(boards)[j] =
                     side == OTH_BLACK ? make_ulonglong2(P, O) : make_ulonglong2(O, P);
                 turn[j] = (uint8_t)side;
@@ -400,10 +347,10 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
                 return;
             }
             if (legal) {
-                const u64 mv = 1ull << kth_bit(legal, pick(key, ply, (u32)__popcll(legal)));
-                const u64 f = flips(mv, P, O);
+                const u64 mv = 1ull << kth_bit(legal, rng.pick((u32)__popcll(legal)));
+                const u64 f = flips_tested(mv, P, O);
                 P |= f | mv;
-                O &= ~f;
+                O = andn(O, f);
             }
             const u64 t = P;
             P = O;
@@ -415,6 +362,47 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
 }
 
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
+
+// launch geometry of the rollout kernel, resolved once per process (device 0 of
+// the calling thread's current device).  Env overrides are tuning knobs for
+// tools/diag only: OTH_ROLLOUT_BLOCKS_PER_CU.
+struct Tuning {
+    unsigned resident_blocks[2];  // per policy
+};
+std::atomic<unsigned long long> g_slot{0};
+
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+const Tuning& tuning() {
+    static Tuning t = [] {
+        Tuning r;
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const void* kern[2] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM>),
+                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY>)};
+        for (int p = 0; p < 2; p++) {
+            int per_cu = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
+            per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu > 0 ? per_cu : 2);
+            r.resident_blocks[p] = (unsigned)(cus * per_cu);
+        }
+        return r;
+    }();
+    return t;
+}
+
+unsigned long long* work_base() {
+    static unsigned long long* p = [] {
+        void* q = nullptr;
+        (void)hipGetSymbolAddress(&q, HIP_SYMBOL(g_work));
+        return reinterpret_cast<unsigned long long*>(q);
+    }();
+    return p;
+}
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int launched() { return status(hipGetLastError()); }
 
@@ -477,14 +465,15 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     a.moves = moves;
     a.hist = (long long*)hist;
     a.n = n;
-    // aim for ~16 waves per CU on 256 CUs, at least 64 games per wave
-    const int64_t target_waves = 256 * 16;
-    int64_t gpw = (n + target_waves - 1) / target_waves;
-    if (gpw < 64) gpw = 64;
-    a.games_per_wave = gpw;
-    const int64_t waves = (n + gpw - 1) / gpw;
-    const unsigned grid = (unsigned)((waves + (kBlock / 64) - 1) / (kBlock / 64));
-    rollout_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(a);
+    const Tuning& t = tuning();
+    const int slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
+    a.work = work_base() + (size_t)slot * kCtrStride;
+    hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
+    if (e != hipSuccess) return status(e);
+    const int64_t max_blocks = (n + kBlock - 1) / kBlock;
+    const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
+    if (policy == OTH_POLICY_GREEDY) rollout_kernel<OTH_POLICY_GREEDY><<<grid, kBlock, 0, (hipStream_t)stream>>>(a);
+    else rollout_kernel<OTH_POLICY_RANDOM><<<grid, kBlock, 0, (hipStream_t)stream>>>(a);
     return launched();
 }
 

@@ -125,6 +125,9 @@ def mix32(x):
     return x
 
 
+LCG_MUL = 0x915F77F5  # 32-bit LCG multiplier (Steele & Vigna 2021 tables)
+
+
 def seed_state(seed):
     return mix64((seed + GOLDEN64) & M64)
 
@@ -133,12 +136,21 @@ def game_key(S, g):
     return mix64((S + g * GOLDEN64) & M64)
 
 
-def ply_rand(key, ply):
-    return mix32((key & M32) ^ mix32(((key >> 32) + ply) & M32))
+class GameRng:
+    """Per-game draw stream: state0 = lo32(key), increment = hi32(key) | 1;
+    each draw advances state = state * LCG_MUL + inc (mod 2^32) and returns it.
+    A uniform pick in [0, n) is (draw * n) >> 32."""
 
+    def __init__(self, key):
+        self.state = key & M32
+        self.inc = (key >> 32) | 1
 
-def pick(key, ply, n):
-    return (ply_rand(key, ply) * n) >> 32
+    def draw(self):
+        self.state = (self.state * LCG_MUL + self.inc) & M32
+        return self.state
+
+    def pick(self, n):
+        return (self.draw() * n) >> 32
 
 
 # ----------------------------------------------------------------------------
@@ -153,7 +165,7 @@ def play(args):
     A side with no legal move passes ('ps'), as the engines do in game_runner.
     """
     seed, g, policy, n_random, bl, wh, turn = args
-    key = game_key(seed_state(seed), g)
+    rng = GameRng(game_key(seed_state(seed), g))
     b = from_bits(bl, wh, turn)
     moves = []
     ply = 0
@@ -162,7 +174,7 @@ def play(args):
         if not puts:
             code = PASS
         elif policy == 0 or ply < n_random:
-            x, y = puts[pick(key, ply, len(puts))]
+            x, y = puts[rng.pick(len(puts))]
             code = x + 8 * y
         else:
             best, bestv = None, None
@@ -188,8 +200,8 @@ def sample_midgame(args):
     attempt = 0
     while True:
         g = i ^ (attempt << 48)
-        key = game_key(S, g)
-        target = 10 + pick(key, 200, 40)
+        rng = GameRng(game_key(S, g))
+        target = 10 + rng.pick(40)  # the first draw picks the stopping ply
         b = Board()
         ply = 0
         ok = False
@@ -201,13 +213,13 @@ def sample_midgame(args):
             if not puts:
                 code = PASS
             else:
-                x, y = puts[pick(key, ply, len(puts))]
+                x, y = puts[rng.pick(len(puts))]
                 code = x + 8 * y
             assert b.put_s(code_to_str(b, code)) >= 0
             ply += 1
         if ok:
             puts = b.puttables(b.turn)
-            x, y = puts[pick(key, ply, len(puts))]
+            x, y = puts[rng.pick(len(puts))]
             bl, wh = to_bits(b)
             return bl, wh, b.turn, ply, x + 8 * y
         attempt += 1
@@ -369,9 +381,10 @@ def main():
 
     # ---------------------------------------------------------------- RNG known answers
     S = seed_state(SEED)
+    r0 = GameRng(game_key(S, 0))
     rng = {"seed": SEED, "seed_state": hex(S),
            "game_keys": [hex(game_key(S, g)) for g in (0, 1, 2, 1 << 20, (1 << 40) + 3)],
-           "ply_rand_g0": [ply_rand(game_key(S, 0), p) for p in range(8)]}
+           "draws_g0": [r0.draw() for _ in range(8)]}
     json.dump(rng, open(os.path.join(OUT, "rng.json"), "w"), indent=1)
     print("fixtures written to", OUT)
 

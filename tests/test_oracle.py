@@ -64,8 +64,8 @@ def test_rng_known_answers():
     keys = [int(k, 16) for k in rng["game_keys"]]
     for g, k in zip((0, 1, 2, 1 << 20, (1 << 40) + 3), keys):
         assert oracle.game_key(rng["seed"], g) == k
-    for p, v in enumerate(rng["ply_rand_g0"]):
-        assert oracle.ply_rand(keys[0], p) == v
+    for i, v in enumerate(rng["draws_g0"]):
+        assert oracle.rng_draw(keys[0], i + 1) == v
 
 
 @pytest.mark.parametrize("name", ROLLOUT_FIXTURES)

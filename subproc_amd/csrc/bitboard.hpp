@@ -53,6 +53,24 @@ __device__ __forceinline__ PairProp pair_prop(u64 pro) {
     return q;
 }
 
+// An empty asm that hides a value's provenance (emits no instruction).  Used on
+// propagators shared between legal-move generation and flips: otherwise hipcc
+// CSEs their complements (one v_not each, kept live) and rewrites every bfi of
+// the flip fills into and + or.
+__device__ __forceinline__ u64 opaque(u64 x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ PairProp opaque(const PairProp& q) {
+    PairProp r;
+    r.pro = opaque(q.pro);
+    r.p2L = opaque(q.p2L);
+    r.p4L = opaque(q.p4L);
+    r.p2R = opaque(q.p2R);
+    r.p4R = opaque(q.p4R);
+    return r;
+}
+
 // occluded fill of `gen` along +S (L) or -S through the pair's propagators:
 // covers distances 0..7
 template <int S, bool L>
@@ -109,14 +127,15 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 // along +d, the opponent run counts iff it is attached to a P disc, i.e. lies in
 // the run set of the opposite direction -d.  No bracket test needed.
 __device__ __forceinline__ u64 flips_at(u64 mv, const Position& s) {
-    u64 f = east_run(mv, s.h.pro) & s.A[1];
-    f = bfi(ks<1, false>(mv, s.h), s.A[0], f);
-    f = bfi(ks<8, true>(mv, s.v), s.A[3], f);
-    f = bfi(ks<8, false>(mv, s.v), s.A[2], f);
-    f = bfi(ks<9, true>(mv, s.d9), s.A[5], f);
-    f = bfi(ks<9, false>(mv, s.d9), s.A[4], f);
-    f = bfi(ks<7, true>(mv, s.d7), s.A[7], f);
-    f = bfi(ks<7, false>(mv, s.d7), s.A[6], f);
+    const PairProp h = opaque(s.h), v = opaque(s.v), d9 = opaque(s.d9), d7 = opaque(s.d7);
+    u64 f = east_run(mv, h.pro) & s.A[1];
+    f = bfi(ks<1, false>(mv, h), s.A[0], f);
+    f = bfi(ks<8, true>(mv, v), s.A[3], f);
+    f = bfi(ks<8, false>(mv, v), s.A[2], f);
+    f = bfi(ks<9, true>(mv, d9), s.A[5], f);
+    f = bfi(ks<9, false>(mv, d9), s.A[4], f);
+    f = bfi(ks<7, true>(mv, d7), s.A[7], f);
+    f = bfi(ks<7, false>(mv, d7), s.A[6], f);
     return f;
 }
 

@@ -87,19 +87,27 @@ __device__ __forceinline__ u64 ks(u64 gen, const PairProp& q) {
 // from src through Oi, minus src.
 __device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, (src << 1) + Oi); }
 
+// 64-bit bit reversal (two v_bfrev_b32, halves swapped): square sq <-> 63 - sq,
+// which turns the west ray into an east ray.
+__device__ __forceinline__ u64 rev64(u64 x) {
+    return ((u64)__builtin_bitreverse32((u32)x) << 32) | __builtin_bitreverse32((u32)(x >> 32));
+}
+
 // All propagators + attached runs of one position (mover P, opponent O).
 // A[i]: opponent discs reachable from a P disc along direction i through
 // opponent discs only (board.py:124-139's "hostile" runs, seen from P).
 // Direction index i: 0:+1 1:-1 2:+8 3:-8 4:+9 5:-9 6:+7 7:-7
 struct Position {
-    PairProp h, v, d9, d7;
+    PairProp v, d9, d7;  // the horizontal pair needs no propagators (carry tricks)
+    u64 Oi, rOi;          // inner opponent discs, and bit-reversed
     u64 A[8];
     u64 legal;  // Board.puttables as a mask (board.py:46-52)
 };
 
 __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     const u64 Oi = O & INNER_FILES;
-    s.h = pair_prop<1>(Oi);
+    s.Oi = Oi;
+    s.rOi = rev64(Oi);
     s.v = pair_prop<8>(O);
     s.d9 = pair_prop<9>(Oi);
     s.d7 = pair_prop<7>(Oi);
@@ -107,8 +115,9 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     // carry from each P disc through its adjacent run of inner opponent discs
     // and clears exactly those run bits: A = Oi & ~(Oi + (P << 1)).
     s.A[0] = east_run(P, Oi);
-    // the other fills from P stay inside P | O, so "minus P" is "and O"
-    s.A[1] = ks<1, false>(P, s.h) & O;
+    // west (-1): the same on the bit-reversed board
+    s.A[1] = rev64(east_run(rev64(P), s.rOi));
+    // the Kogge-Stone fills from P stay inside P | O, so "minus P" is "and O"
     s.A[2] = ks<8, true>(P, s.v) & O;
     s.A[3] = ks<8, false>(P, s.v) & O;
     s.A[4] = ks<9, true>(P, s.d9) & O;
@@ -127,9 +136,9 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 // along +d, the opponent run counts iff it is attached to a P disc, i.e. lies in
 // the run set of the opposite direction -d.  No bracket test needed.
 __device__ __forceinline__ u64 flips_at(u64 mv, const Position& s) {
-    const PairProp h = opaque(s.h), v = opaque(s.v), d9 = opaque(s.d9), d7 = opaque(s.d7);
-    u64 f = east_run(mv, h.pro) & s.A[1];
-    f = bfi(ks<1, false>(mv, h), s.A[0], f);
+    const PairProp v = opaque(s.v), d9 = opaque(s.d9), d7 = opaque(s.d7);
+    u64 f = east_run(mv, opaque(s.Oi)) & s.A[1];
+    f = bfi(rev64(east_run(rev64(mv), opaque(s.rOi))), s.A[0], f);
     f = bfi(ks<8, true>(mv, v), s.A[3], f);
     f = bfi(ks<8, false>(mv, v), s.A[2], f);
     f = bfi(ks<9, true>(mv, d9), s.A[5], f);

@@ -197,7 +197,7 @@ struct RolloutArgs {
 __device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
 #endif
 
-template <int POLICY>
+template <int POLICY, bool RECORD>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
 #ifdef OTH_DIAG
     const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
                 P = side == OTH_BLACK ? s0.x : s0.y;
                 O = side == OTH_BLACK ? s0.y : s0.x;
             }
-            if (a.moves) {
+            if (RECORD) {
                 uint4* mrec = reinterpret_cast<uint4*>(a.moves + g * OTH_MOVES_STRIDE);
 #pragma unroll
                 for (int q = 0; q < OTH_MOVES_STRIDE / 16; q++) mrec[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
                 continue;
             }
             if (passed) {
-                if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
+                if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
                 ply++;
                 passed = false;
             }
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
             }
             const u64 mv = 1ull << sq;
             const u64 f = flips_at(mv, pos);
-            if (a.moves && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
+            if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
             const u64 np = andn(O, f);
             O = P | f | mv;
             P = np;
@@ -382,8 +382,8 @@ const Tuning& tuning() {
         int dev = 0, cus = 256;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const void* kern[2] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM>),
-                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY>)};
+        const void* kern[2] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM, false>),
+                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY, false>)};
         for (int p = 0; p < 2; p++) {
             int per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
@@ -472,8 +472,14 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     if (e != hipSuccess) return status(e);
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
-    if (policy == OTH_POLICY_GREEDY) rollout_kernel<OTH_POLICY_GREEDY><<<grid, kBlock, 0, (hipStream_t)stream>>>(a);
-    else rollout_kernel<OTH_POLICY_RANDOM><<<grid, kBlock, 0, (hipStream_t)stream>>>(a);
+    hipStream_t st = (hipStream_t)stream;
+    if (policy == OTH_POLICY_GREEDY) {
+        if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, 0, st>>>(a);
+        else rollout_kernel<OTH_POLICY_GREEDY, false><<<grid, kBlock, 0, st>>>(a);
+    } else {
+        if (moves) rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, 0, st>>>(a);
+        else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
+    }
     return launched();
 }
 

@@ -28,8 +28,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md
+# VALU issue ceiling for this code's instruction mix: every VALU instruction of
+# these kernels occupies its SIMD for one quad-cycle (measured: SQ_ACTIVE_INST_VALU
+# == SQ_INSTS_VALU; tools/diag/valu_rate*.cpp), 1024 SIMDs at the 2.4 GHz max clock
+VALU_PEAK_WINSTR = 1024 * 2.4e9 / 4
 STEP_BYTES = 52  # algorithmic bytes per oth_step: in 16+1+1, out 16+1+8+8+1
 ROLLOUT_BYTES_PER_GAME = 18  # final board 16 + diff 1 + plies 1 written; opening generated in-kernel
+
+
+def load_profile():
+    """Per-launch PMC figures of the newest committed round profile
+    (profiles/rNN_profile_summary.json, made by tools/profile_round.sh)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_profile_summary.json")))
+    if not files:
+        return None, {}
+    with open(files[-1]) as f:
+        return os.path.basename(files[-1]), json.load(f).get("kernels", {})
+
+
+def profile_entry(kernels, name, grid=None):
+    for k, e in kernels.items():
+        kn, g = k.rsplit("@", 1)
+        if kn == name and (grid is None or int(g) == grid):
+            return e
+    return None
 
 
 def parse():
@@ -57,7 +81,10 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # BENCH_FORCE_DIST=1 runs the RCCL path (barrier, per-step histogram
+    # all-reduce, max-over-ranks timing) even at world size 1
+    use_dist = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     from subproc_amd import ops
@@ -66,12 +93,12 @@ def main():
     stream = torch.cuda.current_stream()
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
     def max_over_ranks(x):
-        if world == 1:
+        if not use_dist:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -91,17 +118,27 @@ def main():
         lib = _lib.load()
         pid = 0 if policy == "random" else 1
 
+        pending = []
+
         def one_step(s):
             # bench step s plays global game ids [(s*world + rank)*n, +n): fresh games every step
             h = hists[s]
             _lib.check(lib.oth_rollout(None, None, args.seed, (s * world + rank) * n, pid, 10, fb.data_ptr(),
                                        df.data_ptr(), pl.data_ptr(), None, h.data_ptr(), n, stream.cuda_stream),
                        "oth_rollout")
-            if world > 1:
-                dist.all_reduce(h, op=dist.ReduceOp.SUM)  # config 4: the one collective, inside the timed region
+            if use_dist:
+                # config 4: the one collective.  Async on RCCL's stream, so it overlaps the
+                # next step's rollout (each step owns its histogram row); all are waited
+                # for inside the timed region.
+                pending.append(dist.all_reduce(h, op=dist.ReduceOp.SUM, async_op=True))
+
+        def drain():
+            while pending:
+                pending.pop().wait()
 
         for s in range(args.warmup):
             one_step(s)
+        drain()
         barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
@@ -109,11 +146,12 @@ def main():
         for s in range(args.warmup, args.warmup + args.steps):
             one_step(s)
         ev1.record(stream)
+        drain()
         barrier()
         t1 = time.perf_counter()
         elapsed = max_over_ranks(t1 - t0)
         kern_ms = ev0.elapsed_time(ev1) / args.steps  # stream-ordered: the rollout launch (+ all-reduce at N>1)
-        timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) at N>1
+        timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) when distributed
         env_steps = int(timed[132])
         games = n * world * args.steps
         value = env_steps / elapsed
@@ -127,11 +165,20 @@ def main():
                            "env_steps_per_game": env_steps / games})
         per_launch_games = n
         achieved = per_launch_games * ROLLOUT_BYTES_PER_GAME / (kern_ms * 1e-3) / 1e9
+        kname = "rollout_kernel<%d, false>" % pid
+        pfile, kernels = load_profile()
+        prof = profile_entry(kernels, kname) if n == 1 << 20 else None
         out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                           "kernel": "rollout_kernel", "kernel_ms": kern_ms,
-                           "note": "integer-VALU-bound kernel: %d algorithmic B/game written; see valu figures in "
-                                   "DESIGN.md" % ROLLOUT_BYTES_PER_GAME}
+                           "frac": achieved / HBM_PEAK_GBS,
+                           "traffic": prof.get("hbm_bytes") if prof else None,
+                           "kernel": kname, "launch_ms": kern_ms, "profile": pfile if prof else None,
+                           "note": "%d algorithmic B/game written (final board, diff, plies); the kernel is "
+                                   "integer-VALU-bound, see 'valu'" % ROLLOUT_BYTES_PER_GAME}
+        if prof and "SQ_INSTS_VALU" in prof:
+            va = prof["SQ_INSTS_VALU"] / (kern_ms * 1e-3)
+            out["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s",
+                           "frac": va / VALU_PEAK_WINSTR, "instr_per_launch": prof["SQ_INSTS_VALU"],
+                           "busy_pmc": prof.get("valu_busy"), "clock_ghz_pmc": prof.get("clock_ghz")}
     else:
         out.update(_bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks))
 
@@ -148,7 +195,7 @@ def main():
         out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
@@ -180,10 +227,18 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
     kern_ms = ev0.elapsed_time(ev1) / K
     steps = n * K * world
     achieved = n * STEP_BYTES / (kern_ms * 1e-3) / 1e9
-    return {"metric": "env-steps/sec (batched step)", "value": steps / elapsed, "unit": "env-steps/s",
-            "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "step_kernel"}}
+    pfile, kernels = load_profile()
+    prof = profile_entry(kernels, "step_kernel", n)
+    r = {"metric": "env-steps/sec (batched step)", "value": steps / elapsed, "unit": "env-steps/s",
+         "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
+         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("hbm_bytes") if prof else None,
+                      "kernel": "step_kernel", "profile": pfile if prof else None}}
+    if prof and "SQ_INSTS_VALU" in prof:
+        va = prof["SQ_INSTS_VALU"] / (kern_ms * 1e-3)
+        r["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s", "frac": va / VALU_PEAK_WINSTR,
+                     "busy_pmc": prof.get("valu_busy")}
+    return r
 
 
 def _bench_greedy(ops, torch, dev, stream, args):

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Per-kernel, per-launch summary of a tools/profile_round.sh output directory.
+
+Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
+  * FETCH_SIZE / WRITE_SIZE are in KiB per dispatch;
+  * on gfx950 FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced
+    streaming read: fetch_bytes_corrected = 2 * FETCH_SIZE * 1024 (an upper
+    estimate for narrower accesses, which the guide leaves uncalibrated);
+  * SQ_ACTIVE_INST_VALU counts quad-cycles; SQ_BUSY_CYCLES is summed over the
+    32 shader engines: VALU busy = 4 * ACTIVE_INST_VALU / (1024 SIMDs * BUSY/32).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+N_SE = 32
+N_SIMD = 1024
+
+
+def short(name):
+    for k in ("rollout_kernel<0, false>", "rollout_kernel<1, false>", "rollout_kernel<0, true>",
+              "rollout_kernel<1, true>", "step_kernel", "legal_kernel", "result_kernel", "reset_kernel",
+              "sample_midgame_kernel"):
+        if k in name:
+            return k
+    return None
+
+
+def pmc(d):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k is None:
+                continue
+            # key by grid size too: step_kernel runs at two batch sizes
+            out[(k, int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main(d):
+    stats = {}
+    for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Name"])
+            if k:
+                stats[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                            "max_ns": float(r["MaxNs"])}
+    trace = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k:
+                trace[(k, int(r.get("Grid_Size") or r["Grid_Size_X"]))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    counters = {}
+    for sub in ("fetch", "write", "sq", "grbm"):
+        for key, cs in pmc(os.path.join(d, sub)).items():
+            for c, v in cs.items():
+                counters.setdefault(key, {})[c] = sum(v) / len(v)
+    out = {"kernels": {}}
+    for (k, grid), cs in sorted(counters.items()):
+        e = {"grid_threads": grid}
+        durs = trace.get((k, grid))
+        if durs:
+            e["launches"] = len(durs)
+            e["avg_ns"] = sum(durs) / len(durs)
+        if "FETCH_SIZE" in cs:
+            e["fetch_bytes_raw"] = cs["FETCH_SIZE"] * 1024
+            e["fetch_bytes_corrected"] = 2 * cs["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in cs:
+            e["write_bytes"] = cs["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE"):
+            if c in cs:
+                e[c] = cs[c]
+        if "SQ_ACTIVE_INST_VALU" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"] > 0:
+            e["valu_busy"] = 4 * cs["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cs["SQ_BUSY_CYCLES"] / N_SE)
+        if "GRBM_GUI_ACTIVE" in cs and durs:
+            e["clock_ghz"] = cs["GRBM_GUI_ACTIVE"] / 8 / (sum(durs) / len(durs))
+        out["kernels"][f"{k}@{grid}"] = e
+    out["kernel_stats"] = stats
+    json.dump(out, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -42,6 +42,9 @@ extern "C" {
 #define OTH_PASS 64
 #define OTH_HIST_BINS 133   /* [0..128] diff+64, 129 black wins, 130 white wins, 131 draws, 132 total plies */
 #define OTH_MOVES_STRIDE 128 /* bytes per game in the optional rollout move record */
+#define OTH_POS_STRIDE 129   /* positions per game in a replay (start + one per recorded move) */
+#define OTH_BOOK_LINE 67     /* bytes per serialize_str() line incl. '\n' */
+#define OTH_FEATURES 10      /* features per position of oth_features */
 
 #define OTH_POLICY_RANDOM 0
 #define OTH_POLICY_GREEDY 1  /* 1-ply minimise opponent mobility, ties -> lowest square */
@@ -96,6 +99,30 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
  * (DESIGN.md §Synthetic mid-game positions).  nturn may be NULL. */
 int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn,
                        uint8_t* nturn, uint8_t* move, int64_t n, void* stream);
+
+/* ---- SURVEY.md §8f "next" rows ------------------------------------------ */
+
+/* Book emitter, step 1: replay recorded move codes (a rollout's `moves`
+ * record, or any put_s code list) into every recorded position, as
+ * GameRunner records them (game_runner.py:169-184: after Board() and after each
+ * put_s, put_s semantics incl. ignored illegal moves).  Game i's position p
+ * (0 <= p <= plies[i], plies capped at OTH_MOVES_STRIDE) goes to row
+ * i*OTH_POS_STRIDE + p of pos_boards (rows, 2 x u64), pos_turn and pos_end
+ * (is_game_over(), board.py:57-58; game_recorder.py:111).  start/start_turn
+ * NULL = opening.  pos_turn / pos_end may be NULL. */
+int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+               uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream);
+
+/* Book emitter, step 2: serialize_str() (board.py:214-243: 64 chars O/X/-,
+ * ' ', side O/X/-) + '\n' for n consecutive positions, concatenated into
+ * out[n * OTH_BOOK_LINE] -- the body of FlatFileRecorder's file
+ * (game_recorder.py:67-76). */
+int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream);
+
+/* Learner features: counts() of parameter_progress_position_moves_learn.py:5-17
+ * for side[i] in {1 = 'O', 2 = 'X'}: out[i*10 + 0] = 64 - n_empty,
+ * [1] = n_puttable_for(side), [2..9] = mask_count(side, region mask a..h). */
+int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,12 +36,14 @@ def lib():
         L.oracle_result.argtypes = [P, P, P, P, P, I64]
         L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I]
         L.oracle_sample_midgame.argtypes = [U64, U64, P, P, P, P, I64]
+        L.oracle_features.argtypes = [P, P, P, I64]
+        L.oracle_replay.argtypes = [P, P, P, P, P, P, P, I64]
         L.oracle_game_key.argtypes = [U64, U64]
         L.oracle_game_key.restype = U64
         L.oracle_rng_draws.argtypes = [U64, ctypes.c_uint32]
         L.oracle_rng_draws.restype = ctypes.c_uint32
         for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
-                  "oracle_sample_midgame"):
+                  "oracle_sample_midgame", "oracle_features", "oracle_replay"):
             getattr(L, f).restype = I
         _lib = L
     return _lib
@@ -116,6 +118,34 @@ def sample_midgame(n, seed, index0=0):
     t, nt, m = (np.empty(n, np.uint8) for _ in range(3))
     lib().oracle_sample_midgame(seed, index0, _p(b), _p(t), _p(nt), _p(m), n)
     return dict(boards=b, turn=t, nturn=nt, move=m)
+
+
+def features(boards, side):
+    boards = _boards(boards)
+    side = np.ascontiguousarray(side, np.uint8)
+    out = np.empty((len(boards), 10), np.uint8)
+    lib().oracle_features(_p(boards), _p(side), _p(out), len(boards))
+    return out
+
+
+def replay(moves, plies, start=None, start_turn=None):
+    moves = np.ascontiguousarray(moves, np.uint8)
+    plies = np.ascontiguousarray(plies, np.uint8)
+    n = len(plies)
+    start = None if start is None else _boards(start)
+    st = None if start_turn is None else np.ascontiguousarray(start_turn, np.uint8)
+    pos = np.zeros((n, MOVES_STRIDE + 1, 2), np.uint64)
+    t = np.zeros((n, MOVES_STRIDE + 1), np.uint8)
+    e = np.zeros((n, MOVES_STRIDE + 1), np.uint8)
+    lib().oracle_replay(_p(start), _p(st), _p(moves), _p(plies), _p(pos), _p(t), _p(e), n)
+    return dict(boards=pos, turn=t, end=e)
+
+
+def serialize_str(black, white, turn):
+    """board.py:214-243 restated for the checker (row-major, O = Black, X = White)."""
+    black, white = int(black), int(white)
+    b = "".join("O" if black >> i & 1 else "X" if white >> i & 1 else "-" for i in range(64))
+    return b + " " + ("O" if turn == 1 else "X" if turn == 2 else "-")
 
 
 def game_key(seed, g):

@@ -360,6 +360,54 @@ int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint
     return 0;
 }
 
+/* mask_count, board.py:74-81 */
+static int mask_count(const Board* s, int color, uint64_t mask) {
+    int ret = 0;
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++)
+            if (((mask >> (j + i * 8)) & 1) && s->b[i][j] == color) ret++;
+    return ret;
+}
+
+/* counts(), parameter_progress_position_moves_learn.py:5-17 (side 1 = 'O', 2 = 'X') */
+int oracle_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n) {
+    static const uint64_t masks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
+                                      0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
+                                      0x0000240000240000ull, 0x0000183C3C180000ull};
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        board_from_bits(&s, boards[2 * i], boards[2 * i + 1], side[i]);
+        int t = side[i];
+        uint8_t* o = out + i * 10;
+        o[0] = (uint8_t)(64 - n_of(&s, Empty));
+        o[1] = (uint8_t)((t == Black || t == White) ? n_puttable_for(&s, t) : 0);
+        for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)mask_count(&s, t, masks[k]);
+    }
+    return 0;
+}
+
+/* recorded positions of a move list, game_runner.py:169-184 (put_s semantics) */
+int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+                  uint64_t* pos, uint8_t* pos_turn, uint8_t* pos_end, int64_t n) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
+        else board_init(&s);
+        int np = plies[i] < MOVES_STRIDE ? plies[i] : MOVES_STRIDE;
+        for (int p = 0;; p++) {
+            int64_t r = i * (MOVES_STRIDE + 1) + p;
+            board_to_bits(&s, &pos[2 * r], &pos[2 * r + 1]);
+            if (pos_turn) pos_turn[r] = (uint8_t)s.turn;
+            if (pos_end) pos_end[r] = (uint8_t)is_game_over(&s);
+            if (p == np) break;
+            if (s.turn == Black || s.turn == White) put_code(&s, moves[i * MOVES_STRIDE + p]);
+        }
+    }
+    return 0;
+}
+
 /* RNG known answers for the fixture check */
 uint64_t oracle_game_key(uint64_t seed, uint64_t g) { return game_key(seed_state(seed), g); }
 uint32_t oracle_rng_draws(uint64_t key, uint32_t count) {

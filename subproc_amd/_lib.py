@@ -15,6 +15,9 @@ OTH_EINVAL = -1000
 BLACK, WHITE, PASS = 1, 2, 64
 HIST_BINS = 133
 MOVES_STRIDE = 128
+POS_STRIDE = 129
+BOOK_LINE = 67
+N_FEATURES = 10
 POLICY_RANDOM, POLICY_GREEDY = 0, 1
 
 # name -> (restype, argtypes); must match include/othello.h exactly
@@ -27,6 +30,9 @@ SIGNATURES = {
     "oth_result": (_I, [_P, _P, _P, _P, _P, _I64, _P]),
     "oth_rollout": (_I, [_P, _P, _U64, _U64, _I, _I, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_sample_midgame": (_I, [_U64, _U64, _P, _P, _P, _P, _I64, _P]),
+    "oth_replay": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_book_text": (_I, [_P, _P, _I64, _P, _P]),
+    "oth_features": (_I, [_P, _P, _P, _I64, _P]),
 }
 
 

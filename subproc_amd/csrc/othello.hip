@@ -80,6 +80,7 @@ __device__ __forceinline__ u32 greedy_move(const Position& s, u64 P, u64 O) {
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ u64 moves_of(u64 P, u64 O) { return moves(P, O); }
 
 // ---------------------------------------------------------------------------
 // elementwise kernels
@@ -141,7 +142,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in,
     const bool moved = r >= 0;
     const u32 t_out = moved ? (t ^ 3u) : t;
     // mover after the step: O if the turn toggled
-    if (legal_next) legal_next[i] = valid_turn ? (moved ? moves(O, P) : moves(P, O)) : 0ull;
+    if (legal_next) {
+        // one analysis of whichever side moves next (select the operands, not the results)
+        const u64 nP = moved ? O : P, nO = moved ? P : O;
+        legal_next[i] = valid_turn ? moves(nP, nO) : 0ull;
+    }
     if (boards_out) {
         const u64 nb = black ? P : O, nw = black ? O : P;
         reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(valid_turn ? nb : b.x, valid_turn ? nw : b.y);
@@ -361,6 +366,118 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
     }
 }
 
+// ---------------------------------------------------------------------------
+// §8f row 1: book emitter.  Replay recorded move codes into every recorded
+// position (game_runner.py:169-184 records the board after Board() and after
+// every put_s), with is_game_over per position (game_recorder.py:107-114).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ start,
+                                                        const uint8_t* __restrict__ start_turn,
+                                                        const uint8_t* __restrict__ moves,
+                                                        const uint8_t* __restrict__ plies, u64* __restrict__ pos,
+                                                        uint8_t* __restrict__ pos_turn, uint8_t* __restrict__ pos_end,
+                                                        int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
+    u32 t = OTH_BLACK;
+    if (start) {
+        const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(start)[i];
+        bl = s0.x;
+        wh = s0.y;
+        t = start_turn ? start_turn[i] : OTH_BLACK;
+    }
+    const u32 np = min<u32>(plies[i], OTH_MOVES_STRIDE);
+    const uint8_t* mv = moves + i * OTH_MOVES_STRIDE;
+    ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
+    for (u32 p = 0;; p++) {
+        out[p] = make_ulonglong2(bl, wh);
+        if (pos_turn) pos_turn[i * OTH_POS_STRIDE + p] = (uint8_t)t;
+        if (pos_end) pos_end[i * OTH_POS_STRIDE + p] = (moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0) ? 1 : 0;
+        if (p == np) break;
+        // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
+        const u32 c = mv[p];
+        if (t != OTH_BLACK && t != OTH_WHITE) continue;
+        if (c == OTH_PASS) {
+            t ^= 3u;
+        } else if (c < 64) {
+            const bool black = t == OTH_BLACK;
+            u64 P = black ? bl : wh, O = black ? wh : bl;
+            const u64 m = 1ull << c;
+            if (!((P | O) & m)) {
+                const u64 f = flips_tested(m, P, O);
+                if (f) {
+                    P |= f | m;
+                    O = andn(O, f);
+                    bl = black ? P : O;
+                    wh = black ? O : P;
+                    t ^= 3u;
+                }
+            }
+        }
+    }
+}
+
+// serialize_str (board.py:214-243) + '\n' of record r = 67 bytes.  One thread
+// writes 16 bytes of the concatenated text, so stores are aligned dwordx4.
+constexpr int kLine = 67;
+__device__ __forceinline__ uint8_t book_char(u64 bl, u64 wh, u32 t, u32 col) {
+    if (col < 64) return (bl >> col & 1) ? 'O' : ((wh >> col & 1) ? 'X' : '-');
+    if (col == 64) return ' ';
+    if (col == 65) return t == OTH_BLACK ? 'O' : (t == OTH_WHITE ? 'X' : '-');
+    return '\n';
+}
+__global__ __launch_bounds__(kBlock) void book_text_kernel(const u64* __restrict__ boards,
+                                                           const uint8_t* __restrict__ turn, int64_t n,
+                                                           uint8_t* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t total = n * kLine;
+    const int64_t k0 = j * 16;
+    if (k0 >= total) return;
+    const int64_t r0 = k0 / kLine;
+    const int64_t r1 = min<int64_t>(r0 + 1, n - 1);
+    const ulonglong2 b0 = reinterpret_cast<const ulonglong2*>(boards)[r0];
+    const ulonglong2 b1 = reinterpret_cast<const ulonglong2*>(boards)[r1];
+    const u32 t0 = turn[r0], t1 = turn[r1];
+    const u32 c0 = (u32)(k0 - r0 * kLine);
+    u32 w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const u32 col = c0 + q;
+        const bool second = col >= kLine;
+        const uint8_t ch = second ? book_char(b1.x, b1.y, t1, col - kLine) : book_char(b0.x, b0.y, t0, col);
+        w[q >> 2] |= (u32)ch << (8 * (q & 3));
+    }
+    if (k0 + 16 <= total) {
+        *reinterpret_cast<uint4*>(out + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int q = 0; k0 + q < total; q++) out[k0 + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// §8f row 2: learner features, counts() of parameter_progress_position_moves_learn.py:5-17:
+// (64 - n_empty, n_puttable_for(side), mask_count(side, m) for the 8 region masks)
+// ---------------------------------------------------------------------------
+__constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
+                                    0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
+                                    0x0000240000240000ull, 0x0000183C3C180000ull};
+__global__ __launch_bounds__(kBlock) void features_kernel(const u64* __restrict__ boards,
+                                                          const uint8_t* __restrict__ side,
+                                                          uint8_t* __restrict__ out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards)[i];
+    const u32 sd = side[i];
+    const u64 mine = sd == OTH_BLACK ? b.x : (sd == OTH_WHITE ? b.y : ~(b.x | b.y));
+    const u64 theirs = sd == OTH_BLACK ? b.y : b.x;
+    uint8_t* o = out + i * OTH_FEATURES;
+    o[0] = (uint8_t)__popcll(b.x | b.y);
+    o[1] = (uint8_t)((sd == OTH_BLACK || sd == OTH_WHITE) ? __popcll(moves_of(mine, theirs)) : 0);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)__popcll(mine & kRegionMasks[k]);
+}
+
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
 
 // launch geometry of the rollout kernel, resolved once per process (device 0 of
@@ -480,6 +597,31 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
         if (moves) rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
+    return launched();
+}
+
+int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+               uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!moves || !plies || !pos_boards))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    replay_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(start, start_turn, moves, plies, pos_boards,
+                                                                     pos_turn, pos_end, n);
+    return launched();
+}
+
+int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream) {
+    if (n < 0 || (n > 0 && (!boards || !turn || !out))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    const int64_t threads = (n * kLine + 15) / 16;
+    book_text_kernel<<<blocks_for(threads), kBlock, 0, (hipStream_t)stream>>>(boards, turn, n,
+                                                                             reinterpret_cast<uint8_t*>(out));
+    return launched();
+}
+
+int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    features_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards, side, out, n);
     return launched();
 }
 

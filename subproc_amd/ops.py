@@ -20,12 +20,14 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import BLACK, HIST_BINS, MOVES_STRIDE, PASS, POLICY_GREEDY, POLICY_RANDOM, WHITE, check
+from ._lib import (BLACK, BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, PASS, POLICY_GREEDY, POLICY_RANDOM,
+                   POS_STRIDE, WHITE, check)
 
 StepResult = namedtuple("StepResult", "boards turn flips legal_next ret")
 Result = namedtuple("Result", "n_black n_white diff terminal")
 RolloutResult = namedtuple("RolloutResult", "final_boards diff plies moves hist")
 Positions = namedtuple("Positions", "boards turn nturn move")
+Replay = namedtuple("Replay", "boards turn end")
 
 _POLICIES = {"random": POLICY_RANDOM, "greedy": POLICY_GREEDY, POLICY_RANDOM: POLICY_RANDOM,
              POLICY_GREEDY: POLICY_GREEDY}
@@ -185,6 +187,51 @@ def sample_midgame(n, seed, index0=0, device="cuda"):
     return Positions(b, t, nt, m)
 
 
+def replay(moves, plies, start=None, start_turn=None):
+    """Every recorded position of n games (GameRunner records the board after
+    Board() and after each put_s, game_runner.py:169-184).  Returns Replay with
+    boards (n, 129, 2) int64, turn (n, 129) uint8, end (n, 129) uint8 =
+    is_game_over(); game i's positions are rows 0..plies[i]."""
+    n = moves.shape[0]
+    pm = _dev(moves, "moves", torch.uint8, (n, MOVES_STRIDE))
+    pp = _dev(plies, "plies", torch.uint8, (n,))
+    ps = _opt(start, "start", torch.int64, (n, 2))
+    pst = _opt(start_turn, "start_turn", torch.uint8, (n,))
+    dev = moves.device
+    b = torch.zeros((n, POS_STRIDE, 2), dtype=torch.int64, device=dev)
+    t = torch.zeros((n, POS_STRIDE), dtype=torch.uint8, device=dev)
+    e = torch.zeros((n, POS_STRIDE), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        check(_lib.load().oth_replay(ps, pst, pm, pp, b.data_ptr(), t.data_ptr(), e.data_ptr(), n, _stream()),
+              "oth_replay")
+    return Replay(b, t, e)
+
+
+def book_text(boards, turn):
+    """serialize_str() + newline of each position (board.py:214-243), concatenated:
+    a uint8 tensor of n * 67 bytes on the device."""
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    pt = _dev(turn, "turn", torch.uint8, (n,))
+    out = torch.empty(n * BOOK_LINE, dtype=torch.uint8, device=boards.device)
+    with torch.cuda.device(boards.device):
+        check(_lib.load().oth_book_text(pb, pt, n, out.data_ptr(), _stream()), "oth_book_text")
+    return out
+
+
+def features(boards, side):
+    """counts() of parameter_progress_position_moves_learn.py:5-17 per position
+    for side 1 ('O' = Black) / 2 ('X' = White): (n, 10) uint8 =
+    (64 - n_empty, n_puttable_for(side), 8 region mask_counts)."""
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    ps = _dev(side, "side", torch.uint8, (n,))
+    out = torch.empty((n, N_FEATURES), dtype=torch.uint8, device=boards.device)
+    with torch.cuda.device(boards.device):
+        check(_lib.load().oth_features(pb, ps, out.data_ptr(), n, _stream()), "oth_features")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # host <-> device conversion helpers (uint64 bit patterns)
 # ---------------------------------------------------------------------------
@@ -199,5 +246,6 @@ def from_numpy_u64(a, device="cuda"):
     return torch.from_numpy(a.view(np.int64).copy()).to(device)
 
 
-__all__ = ["reset", "legal", "step", "result", "rollout", "sample_midgame", "to_numpy_u64", "from_numpy_u64",
+__all__ = ["reset", "legal", "step", "result", "rollout", "sample_midgame", "replay", "book_text", "features",
+           "to_numpy_u64", "from_numpy_u64",
            "StepResult", "Result", "RolloutResult", "Positions", "BLACK", "WHITE", "PASS", "HIST_BINS"]

@@ -54,6 +54,32 @@ def load_reference_board():
 
 RB = load_reference_board()
 Board = RB["Board"]
+
+
+def load_reference_counts():
+    """parameter_progress_position_moves_learn.counts (and parameter.board_from_a_book)
+    from the reference, exec'd against the shimmed board module.  Both files are
+    valid Python 3 as they stand; nothing is copied."""
+    import types
+    mod_board = types.ModuleType("board")
+    mod_board.__dict__.update(RB)
+    saved = {k: sys.modules.get(k) for k in ("board", "parameter")}
+    sys.modules["board"] = mod_board
+    try:
+        mod_param = types.ModuleType("parameter")
+        exec(compile(open("/root/reference/parameter.py").read(), "reference_parameter.py", "exec"),
+             mod_param.__dict__)
+        sys.modules["parameter"] = mod_param
+        ns = {"__name__": "reference_ppml"}
+        exec(compile(open("/root/reference/parameter_progress_position_moves_learn.py").read(),
+                     "reference_ppml.py", "exec"), ns)
+        return ns["counts"]
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
 Black, White, Empty = RB["Black"], RB["White"], RB["Empty"]
 
 
@@ -378,6 +404,30 @@ def main():
                         black=u64([s[0] for s in sm]), white=u64([s[1] for s in sm]),
                         turn=np.array([s[2] for s in sm], np.uint8), nturn=np.array([s[3] for s in sm], np.uint8),
                         move=np.array([s[4] for s in sm], np.uint8))
+
+    # ---------------------------------------------------------------- books (§8f row 1) + features (row 2)
+    counts = load_reference_counts()
+    z = np.load(os.path.join(OUT, "rollout_random.npz"))
+    zm = np.load(os.path.join(OUT, "rollout_random_from_mid.npz"))
+    books = []
+    for src, g in [(z, i) for i in range(12)] + [(zm, i) for i in range(4)]:
+        b = from_bits(int(src["start_black"][g]), int(src["start_white"][g]), int(src["start_turn"][g]))
+        lines = [b.serialize_str()]  # FlatFileRecorder.add after Board() (game_runner.py:169-170)
+        records = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                    "end": b.is_game_over()}]
+        feats = []
+        for code in src["moves"][g]:
+            if code == 255:
+                break
+            assert b.put_s(code_to_str(b, int(code))) >= 0
+            lines.append(b.serialize_str())
+            records.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                            "end": b.is_game_over()})
+        for rec in records:
+            feats.append([list(counts(rec, "O")), list(counts(rec, "X"))])
+        books.append({"source": "rollout_random" if src is z else "rollout_random_from_mid", "game": g,
+                      "lines": lines, "records": records, "counts": feats})
+    json.dump(books, open(os.path.join(OUT, "books.json"), "w"))
 
     # ---------------------------------------------------------------- RNG known answers
     S = seed_state(SEED)

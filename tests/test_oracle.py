@@ -105,3 +105,22 @@ def test_rollout_split_invariance():
     b2 = oracle.rollout(56, 7, 1040)
     np.testing.assert_array_equal(a["final_boards"], np.concatenate([b1["final_boards"], b2["final_boards"]]))
     np.testing.assert_array_equal(a["hist"], b1["hist"] + b2["hist"])
+
+
+def test_books_and_features_vs_reference():
+    """Book lines/records and counts() features from board.py + the reference
+    learner module (tests/golden/books.json) reproduced by the oracle."""
+    zs = {n: load_npz(n + ".npz") for n in ("rollout_random", "rollout_random_from_mid")}
+    for bk in load_json("books.json"):
+        z, g = zs[bk["source"]], bk["game"]
+        rp = oracle.replay(z["moves"][g:g + 1], z["plies"][g:g + 1],
+                           np.stack([z["start_black"], z["start_white"]], 1)[g:g + 1], z["start_turn"][g:g + 1])
+        p = int(z["plies"][g])
+        assert len(bk["lines"]) == p + 1
+        for k in range(p + 1):
+            bl, wh = rp["boards"][0, k]
+            assert oracle.serialize_str(bl, wh, rp["turn"][0, k]) == bk["lines"][k]
+            assert bool(rp["end"][0, k]) == bk["records"][k]["end"]
+            for side, ref in ((1, bk["counts"][k][0]), (2, bk["counts"][k][1])):
+                f = oracle.features(np.array([[bl, wh]], np.uint64), [side])[0]
+                assert list(f) == ref, (bk["game"], k, side)

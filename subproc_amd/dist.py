@@ -60,3 +60,20 @@ def hist_summary(hist):
                 black_win_rate=h[129] / games if games else 0.0, white_win_rate=h[130] / games if games else 0.0,
                 avg_diff=sum((d - 64) * h[d] for d in range(129)) / games if games else 0.0,
                 min_diff=min(diffs) if diffs else 0, max_diff=max(diffs) if diffs else 0)
+
+
+def batch_stats_payload(hist, black_name="black", white_name="white", params_used=""):
+    """The payload LearnBase.store_batch_stats stores (learn_base.py:91-109),
+    computed from the GPU histogram instead of per-book Board.deserialize:
+    '<black>_win_rate', '<white>_win_rate', min/max/avg disc diff, and the
+    sorted per-game disc diffs (expanded from the histogram counts).
+    Wins use the correct rule: white wins iff white_discs > black_discs
+    (learn_base.py:77 compares against the running black-win count)."""
+    h = hist.tolist() if isinstance(hist, torch.Tensor) else list(hist)
+    s = hist_summary(h)
+    if s["games"] == 0:
+        raise ValueError("empty batch (learn_base.py divides by len(books))")
+    diffs = [d - 64 for d in range(129) for _ in range(h[d])]
+    return {black_name + "_win_rate": s["black_win_rate"], white_name + "_win_rate": s["white_win_rate"],
+            "min_disc_diff": s["min_diff"], "max_disc_diff": s["max_diff"], "avg_disc_diff": s["avg_diff"],
+            "params_used": params_used, "diffs": diffs}

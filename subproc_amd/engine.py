@@ -1,0 +1,112 @@
+"""Edax-protocol engine backed by the GPU env.
+
+The reference drives external engines through pipes with the Player class
+(game_runner.py:9-102).  This module answers exactly the commands Player sends,
+so ``proc_a_path = python -m subproc_amd.engine --policy greedy`` plugs a GPU
+policy into GameRunner unchanged:
+
+  init          -> 1 line                                   (game_runner.py:35-39)
+  go            -> 3 lines; joined they match
+                   ">(.+) plays [WB]?([a-zA-Z][0-9]|PS)"     (game_runner.py:19-33)
+                   and the engine plays that move on its board
+  <move>        -> 3 lines matching "(.+) play ([a-zA-Z][0-9]|PS|ps)"  (game_runner.py:41-54);
+                   the move ('d3', 'ps', ...) is applied for the side to move
+                   (go_for also sends the engine its OWN randomised moves, 149)
+  verbose p     -> 1 line (parameter description)           (game_runner.py:66-73)
+  verbose 1     -> 13 lines of board display                 (game_runner.py:75-91)
+  verbose 0     -> nothing
+  quit          -> 1 line, exit                              (game_runner.py:56-64)
+
+Rules and move generation run on the GPU through the drop-in Board
+(subproc_amd.board); the move choice is the env's policy: "random" (uniform
+over legal moves, seeded) or "greedy" (minimise the opponent's mobility, ties
+to the first move in puttables order).
+"""
+import argparse
+import random
+import sys
+
+from . import board as gboard
+from .codec import handstr_from_coord
+
+
+class Engine:
+    def __init__(self, name="GPU", policy="greedy", seed=0):
+        self.name = name
+        self.policy = policy
+        self.rng = random.Random(seed)
+        self.board = gboard.Board()
+
+    def choose(self):
+        b = self.board
+        puts = b.puttables(b.turn)
+        if not puts:
+            return "PS"
+        if self.policy == "random":
+            x, y = puts[self.rng.randrange(len(puts))]
+            return handstr_from_coord(x, y)
+        best, bestv = None, None
+        opp = b.hostile(b.turn)
+        for (x, y) in puts:
+            c = gboard.Board()
+            c.board = b.board
+            c.turn = b.turn
+            c.put_s(handstr_from_coord(x, y))
+            v = c.n_puttable_for(opp)
+            if bestv is None or v < bestv:
+                best, bestv = (x, y), v
+        return handstr_from_coord(*best)
+
+    def handle(self, line, out):
+        cmd = line.strip()
+        if cmd == "init":
+            self.board = gboard.Board()
+            out("init done")
+        elif cmd == "go":
+            mv = self.choose()
+            color = "B" if self.board.turn == gboard.Black else "W"
+            self.board.put_s(mv.lower() if mv != "PS" else "PS")
+            out("")
+            out(">%s plays %s%s" % (self.name, color, mv.upper() if mv != "PS" else "PS"))
+            out("")
+        elif cmd == "verbose p":
+            out("%s policy=%s" % (self.name, self.policy))
+        elif cmd == "verbose 1":
+            text = str(self.board).rstrip("\n").split("\n")
+            text += [""] * (13 - len(text))
+            for t in text[:13]:
+                out(t)
+        elif cmd.startswith("verbose"):
+            pass
+        elif cmd == "quit":
+            out("bye")
+            return False
+        elif cmd:
+            mv = cmd.split()[-1]
+            self.board.put_s(mv)
+            out("")
+            out("%s play %s" % (self.name, mv))
+            out("")
+        return True
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--name", default="GPU")
+    p.add_argument("--policy", choices=["random", "greedy"], default="greedy")
+    p.add_argument("--seed", type=int, default=0)
+    a = p.parse_args(argv)
+    eng = Engine(a.name, a.policy, a.seed)
+
+    def out(s):
+        sys.stdout.write(s + "\n")
+        sys.stdout.flush()
+
+    for line in sys.stdin:
+        if not eng.handle(line, out):
+            break
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -59,3 +59,20 @@ def test_world2_histogram_equals_single_process():
     assert res[0][1] + res[1][1] == total
     s = hist_summary(ref)
     assert s["games"] == total and s["black_wins"] + s["white_wins"] + s["draws"] == total
+
+
+def test_batch_stats_payload_matches_per_book_rule():
+    """learn_base.store_batch_stats quantities from the histogram == the same
+    quantities computed per game from the terminal boards (correct win rule)."""
+    from golden_io import load_npz
+    from subproc_amd.dist import batch_stats_payload
+    z = load_npz("rollout_random.npz")
+    r = oracle.rollout(len(z["plies"]), int(z["seed"]), int(z["game_id0"]))
+    nb = np.array([bin(int(b)).count("1") for b in z["final_black"]])
+    nw = np.array([bin(int(w)).count("1") for w in z["final_white"]])
+    d = nb - nw
+    p = batch_stats_payload(r["hist"], "gpuA", "gpuB")
+    assert p["gpuA_win_rate"] == (nb > nw).mean() and p["gpuB_win_rate"] == (nw > nb).mean()
+    assert p["min_disc_diff"] == d.min() and p["max_disc_diff"] == d.max()
+    assert abs(p["avg_disc_diff"] - d.mean()) < 1e-12
+    assert p["diffs"] == sorted(d.tolist())

@@ -1,0 +1,93 @@
+"""The Edax-protocol engine shim (subproc_amd.engine) driven exactly as the
+reference's Player/GameRunner drive an engine (game_runner.py:9-201, restated
+in Python 3 here: the reference is Python 2 and needs the external binaries)."""
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+from subproc_amd import board as gboard  # noqa: E402
+from subproc_amd import codec  # noqa: E402
+
+
+class Player:  # game_runner.py:9-64 protocol
+    def __init__(self, args):
+        self.proc = subprocess.Popen([sys.executable, "-m", "subproc_amd.engine", *args], stdin=subprocess.PIPE,
+                                     stdout=subprocess.PIPE, text=True, bufsize=1)
+        self.name = ""
+
+    def _w(self, s):
+        self.proc.stdin.write(s)
+        self.proc.stdin.flush()
+
+    def go(self):
+        self._w("go\n")
+        out = "".join(self.proc.stdout.readline() for _ in range(3))
+        out = re.sub(r"[\r\n]+", "", out)
+        b = re.findall(r">(.+) plays [WB]?([a-zA-Z][0-9]|PS)", out.rstrip())
+        self.name = b[0][0]
+        return b[0][1]
+
+    def init(self):
+        self._w("init\n")
+        self.proc.stdout.readline()
+
+    def play(self, hand):
+        self._w(hand + "\n")
+        out = "".join(self.proc.stdout.readline() for _ in range(3))
+        a = re.findall(r"(.+) play ([a-zA-Z][0-9]|PS|ps)", out.rstrip())
+        return a[0][1]
+
+    def end_process(self):
+        self._w("quit\n")
+        self.proc.stdout.readline()
+        self.proc.communicate(timeout=60)
+
+
+def play_a_game(black, white):  # game_runner.py:154-201 without randomisation
+    black.init()
+    white.init()
+    b = gboard.Board()
+    record = [b.serialize_str()]
+    moves = []
+    over = b.is_game_over()
+    atk, dfn = black, white
+    while not over:
+        ha = atk.go().lower()
+        assert b.put_s(ha) >= 0, ha
+        moves.append(codec.move_code(ha))
+        record.append(b.serialize_str())
+        dfn.play(ha)
+        over = b.is_game_over()
+        atk, dfn = dfn, atk
+    black.end_process()
+    white.end_process()
+    return b, moves, record
+
+
+@pytest.mark.parametrize("pa,pb", [("greedy", "random"), ("random", "random")])
+def test_engine_plays_full_game(pa, pb):
+    black = Player(["--policy", pa, "--name", "GPU-%s" % pa, "--seed", "1"])
+    white = Player(["--policy", pb, "--name", "GPU-%s" % pb, "--seed", "2"])
+    try:
+        final, moves, record = play_a_game(black, white)
+    finally:
+        for p in (black, white):
+            if p.proc.poll() is None:
+                p.proc.kill()
+    assert final.is_game_over()
+    assert black.name == "GPU-%s" % pa
+    # the game record replays bit-exactly through the oracle (board.py semantics)
+    mv = np.full((1, 128), 255, np.uint8)
+    mv[0, :len(moves)] = moves
+    o = oracle.replay(mv, np.array([len(moves)], np.uint8))
+    for k, line in enumerate(record):
+        bl, wh = o["boards"][0, k]
+        assert oracle.serialize_str(bl, wh, o["turn"][0, k]) == line
+    assert o["end"][0, len(moves)] == 1

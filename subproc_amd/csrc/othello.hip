@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 
 #include "../../include/othello.h"
 #include "bitboard.hpp"
@@ -493,11 +494,25 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-const Tuning& tuning() {
-    static Tuning t = [] {
-        Tuning r;
-        int dev = 0, cus = 256;
-        (void)hipGetDevice(&dev);
+// per-device caches (a process may drive several GPUs); resolved on first use
+constexpr int kMaxDevices = 64;
+struct DeviceState {
+    std::atomic<int> ready{0};
+    Tuning tuning;
+    unsigned long long* work = nullptr;
+};
+DeviceState g_dev[kMaxDevices];
+std::mutex g_dev_mu;
+
+const DeviceState* device_state() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    DeviceState& d = g_dev[dev];
+    if (d.ready.load(std::memory_order_acquire)) return &d;
+    std::lock_guard<std::mutex> lock(g_dev_mu);
+    if (!d.ready.load(std::memory_order_relaxed)) {
+        int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const void* kern[2] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM, false>),
                                reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY, false>)};
@@ -505,20 +520,14 @@ const Tuning& tuning() {
             int per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
             per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu > 0 ? per_cu : 2);
-            r.resident_blocks[p] = (unsigned)(cus * per_cu);
+            d.tuning.resident_blocks[p] = (unsigned)(cus * per_cu);
         }
-        return r;
-    }();
-    return t;
-}
-
-unsigned long long* work_base() {
-    static unsigned long long* p = [] {
         void* q = nullptr;
-        (void)hipGetSymbolAddress(&q, HIP_SYMBOL(g_work));
-        return reinterpret_cast<unsigned long long*>(q);
-    }();
-    return p;
+        if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_work)) != hipSuccess || !q) return nullptr;
+        d.work = reinterpret_cast<unsigned long long*>(q);
+        d.ready.store(1, std::memory_order_release);
+    }
+    return &d;
 }
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int launched() { return status(hipGetLastError()); }
@@ -582,9 +591,11 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     a.moves = moves;
     a.hist = (long long*)hist;
     a.n = n;
-    const Tuning& t = tuning();
+    const DeviceState* ds = device_state();
+    if (!ds) return status(hipErrorInvalidDevice);
+    const Tuning& t = ds->tuning;
     const int slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
-    a.work = work_base() + (size_t)slot * kCtrStride;
+    a.work = ds->work + (size_t)slot * kCtrStride;
     hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
     if (e != hipSuccess) return status(e);
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;

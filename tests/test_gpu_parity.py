@@ -244,3 +244,16 @@ def test_config3_full_size_properties():
     idx = np.arange(0, n, 97)
     o = oracle.rollout(len(idx), 0x5EED, 0)  # contiguous ids 0..len-1
     assert (U(a.final_boards)[:len(idx)] == o["final_boards"]).all()
+
+
+def test_config4_global_histogram_equals_shards():
+    """8,388,608 games in one launch == 8 rank-sized shards (the config-4 layout:
+    rank r plays ids [r*2^20, (r+1)*2^20)), bit-exact: what the RCCL all-reduce
+    of per-rank histograms must reproduce."""
+    n = 1 << 20
+    whole = ops.rollout(8 * n, 0x5EED, 0, device=DEV, want_boards=False, want_diff=False, want_plies=False)
+    acc = torch.zeros_like(whole.hist)
+    for r in range(8):
+        ops.rollout(n, 0x5EED, r * n, hist=acc, device=DEV, want_boards=False, want_diff=False, want_plies=False)
+    assert torch.equal(acc, whole.hist)
+    assert int(whole.hist[:129].sum()) == 8 * n

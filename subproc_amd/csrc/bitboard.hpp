@@ -148,6 +148,57 @@ __device__ __forceinline__ u64 flips_at(u64 mv, const Position& s) {
     return f;
 }
 
+// ---------------------------------------------------------------------------
+// Flips from per-square ray tables (LDS).  For a ray R leaving the move square
+// in increasing bit order, the flipped discs are the run-set squares A on R
+// before the first square of R that is not in A:
+//     x = R & ~A;   flips = R & A & (x - 1)
+// (x != 0 whenever R & A != 0: an attached run ends in a P disc on the same ray).
+// Rays that leave in decreasing bit order use the same identity on the
+// bit-reversed board.  Table rows: 0..2 = rays +8, +9, +7 (normal order),
+// 3..5 = rays -8, -9, -7 stored bit-reversed; 64 squares each (3 KiB).
+constexpr int kRayRows = 6;
+__host__ __device__ inline u64 ray_from(int sq, int dx, int dy) {
+    u64 r = 0;
+    int x = sq & 7, y = sq >> 3;
+    for (;;) {
+        x += dx;
+        y += dy;
+        if (x < 0 || x > 7 || y < 0 || y > 7) break;
+        r |= 1ull << (x + 8 * y);
+    }
+    return r;
+}
+__device__ __forceinline__ void ray_table_init(u64* tab) {
+    for (int e = threadIdx.x; e < kRayRows * 64; e += blockDim.x) {
+        const int row = e >> 6, sq = e & 63;
+        const int dx[6] = {0, 1, -1, 0, -1, 1}, dy[6] = {1, 1, 1, -1, -1, -1};
+        const u64 r = ray_from(sq, dx[row], dy[row]);
+        tab[e] = row < 3 ? r : rev64(r);
+    }
+}
+__device__ __forceinline__ u32 bitop3_and3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80); }
+__device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) {
+    return ((u64)bitop3_and3((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32)) << 32) |
+           bitop3_and3((u32)a, (u32)b, (u32)c);
+}
+__device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
+    const u64 x = andn(R, A);
+    return and3(R, A, x - 1);
+}
+
+// flips of the move at square sq (bit mv): horizontal rays by carry (as in
+// analyse), the other six by the ray tables; A sets from analyse(P, O).
+__device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const Position& s, const u64* tab) {
+    u64 f = east_run(mv, s.Oi) & s.A[1];
+    u64 fr = east_run(rev64(mv), s.rOi) & rev64(s.A[0]);  // west, in reversed space
+    f = or3(f, run_prefix(tab[0 * 64 + sq], s.A[3]), run_prefix(tab[1 * 64 + sq], s.A[5]));
+    f |= run_prefix(tab[2 * 64 + sq], s.A[7]);
+    fr = or3(fr, run_prefix(tab[3 * 64 + sq], rev64(s.A[2])), run_prefix(tab[4 * 64 + sq], rev64(s.A[4])));
+    fr |= run_prefix(tab[5 * 64 + sq], rev64(s.A[6]));
+    return f | rev64(fr);
+}
+
 // legal moves only (no run sets kept) — for child positions / next-state masks
 __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;

@@ -63,14 +63,14 @@ struct GameRng {
 
 // 1-ply greedy: legal move minimising the opponent's mobility on the child,
 // ties -> lowest square (first in puttables order)
-__device__ __forceinline__ u32 greedy_move(const Position& s, u64 P, u64 O) {
+__device__ __forceinline__ u32 greedy_move(const Position& s, u64 P, u64 O, const u64* rays) {
     u32 best = 64, bestv = 1000;
     u64 legal = s.legal;
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         const u64 mv = 1ull << sq;
         legal &= legal - 1;
-        const u64 f = flips_at(mv, s);
+        const u64 f = flips_rays(sq, mv, s, rays);
         const u32 v = (u32)__popcll(moves(andn(O, f), P | f | mv));
         if (v < bestv) {
             bestv = v;
@@ -212,8 +212,10 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
 #endif
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
+    __shared__ u64 rays[kRayRows * 64];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
+    ray_table_init(rays);
     __syncthreads();
 
     const int lane = lane_id();
@@ -287,12 +289,12 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
             }
             u32 sq;
             if (POLICY == OTH_POLICY_GREEDY && (int)ply >= a.n_random) {
-                sq = greedy_move(pos, P, O);
+                sq = greedy_move(pos, P, O, rays);
             } else {
                 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
             }
             const u64 mv = 1ull << sq;
-            const u64 f = flips_at(mv, pos);
+            const u64 f = flips_rays(sq, mv, pos, rays);
             if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
             const u64 np = andn(O, f);
             O = P | f | mv;
@@ -496,6 +498,7 @@ int env_int(const char* name, int dflt) {
 
 // per-device caches (a process may drive several GPUs); resolved on first use
 constexpr int kMaxDevices = 64;
+constexpr int kMaxBlocksPerCu = 5;
 struct DeviceState {
     std::atomic<int> ready{0};
     Tuning tuning;
@@ -519,7 +522,11 @@ const DeviceState* device_state() {
         for (int p = 0; p < 2; p++) {
             int per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
-            per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu > 0 ? per_cu : 2);
+            // 5 blocks of 4 waves per CU (5 waves/SIMD) measured fastest for the
+            // VALU-bound loop (tools/diag/sweep_rollout.sh: 0.471 ms vs 0.484-0.500 at
+            // 6-8); more waves only add batch-tail idle lanes
+            per_cu = per_cu > 0 ? std::min(per_cu, kMaxBlocksPerCu) : 2;
+            per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu);
             d.tuning.resident_blocks[p] = (unsigned)(cus * per_cu);
         }
         void* q = nullptr;

@@ -106,6 +106,32 @@ def test_inplace_step_aliasing():
     assert (U(b2) == U(ref.boards)).all() and (t2.cpu() == ref.turn.cpu()).all()
 
 
+@pytest.mark.parametrize("n,off", [(1, 0), (3, 0), (4, 0), (4093, 0), (4096, 1), (4097, 3), (1023, 2)])
+def test_step_ragged_and_unaligned(n, off):
+    """The step kernel packs 4 boards per thread for aligned arrays (n % 4 tail
+    per board) and runs unaligned views (offset byte arrays) per board: both
+    paths against the oracle, including the uint8 nturn wrap at 255."""
+    rng = np.random.default_rng(n + off)
+    m = n + off
+    occ = rng.integers(0, 2**64, m, dtype=np.uint64) & rng.integers(0, 2**64, m, dtype=np.uint64)
+    col = rng.integers(0, 2**64, m, dtype=np.uint64)
+    nb = np.stack([occ & col, occ & ~col], 1)
+    tt = rng.integers(0, 4, m).astype(np.uint8)
+    mv = rng.integers(0, 66, m).astype(np.uint8)
+    nt0 = rng.choice(np.array([0, 1, 127, 128, 254, 255], np.uint8), m)
+    boards, turn, move = B(nb[:, 0], nb[:, 1])[off:], T(tt)[off:], T(mv)[off:]
+    nturn = T(nt0)[off:]
+    r = ops.step(boards, turn, move, nturn=nturn)
+    o = oracle.step(nb[off:], tt[off:], mv[off:])
+    assert (U(r.boards) == o["boards"]).all()
+    assert (U(r.flips) == o["flips"]).all()
+    assert (U(r.legal_next) == o["legal_next"]).all()
+    assert (r.ret.cpu().numpy() == o["ret"]).all()
+    assert (r.turn.cpu().numpy() == o["turn"]).all()
+    want_nt = (nt0[off:].astype(np.int64) + (o["ret"] >= 0)).astype(np.uint8)
+    np.testing.assert_array_equal(nturn.cpu().numpy(), want_nt)
+
+
 def test_zero_and_bad_args():
     e = torch.empty((0, 2), dtype=torch.int64, device=DEV)
     r = ops.step(e, torch.empty(0, dtype=torch.uint8, device=DEV), torch.empty(0, dtype=torch.uint8, device=DEV))

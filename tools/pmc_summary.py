@@ -20,8 +20,12 @@ def summarise(path, match=None):
 
 
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        for k, cs in summarise(p, "rollout").items():
+    match = "rollout"
+    paths = sys.argv[1:]
+    if paths and paths[0].startswith("--match="):
+        match, paths = paths[0][8:], paths[1:]
+    for p in paths:
+        for k, cs in summarise(p, match).items():
             print(k)
             for c, v in cs.items():
                 print(f"   {c:28s} {v:16.1f}")

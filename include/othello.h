@@ -48,6 +48,17 @@ extern "C" {
 
 #define OTH_POLICY_RANDOM 0
 #define OTH_POLICY_GREEDY 1  /* 1-ply minimise opponent mobility, ties -> lowest square */
+#define OTH_POLICY_EVAL 2    /* 1-ply maximise the mover's linear eval (oth_eval), ties -> lowest square */
+
+/* Linear evaluation weights: int8 [OTH_EVAL_PHASES][OTH_EVAL_FEATURES], row k
+ * for positions whose disc count lies in learner shard k = (0..16, 17..32,
+ * 33..48, 49..64) (progress_position_moves_learn.py:112-113), columns = the 9
+ * non-phase counts() features (n_puttable_for, region masks a..h).  This is the
+ * table ProgressPositionMovesLearn stores and paramgen.py writes (header byte,
+ * 36 int8, trailing 0; paramgen.py:5-19). */
+#define OTH_EVAL_PHASES 4
+#define OTH_EVAL_FEATURES 9
+#define OTH_EVAL_WEIGHTS 36
 
 /* Library version string ("subproc_amd <semver> gfx950"). */
 const char* oth_version(void);
@@ -93,6 +104,15 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
                 int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
                 uint8_t* moves, int64_t* hist, int64_t n, void* stream);
 
+/* oth_rollout with the eval policy: after n_random random plies, each mover
+ * plays the legal move whose child maximises oth_eval(child, mover) under
+ * `weights` (HOST pointer to OTH_EVAL_WEIGHTS int8, copied into the launch, so
+ * the caller may reuse it as soon as the call returns).  Other arguments and
+ * outputs as oth_rollout. */
+int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                     int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                     uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+
 /* Synthetic reachable mid-game positions for the step benchmark (config 2):
  * position index0+j is a random-policy playout of 10..49 plies from the opening
  * at which the mover has >= 1 legal move, plus that mover's random legal move
@@ -123,6 +143,14 @@ int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* 
  * for side[i] in {1 = 'O', 2 = 'X'}: out[i*10 + 0] = 64 - n_empty,
  * [1] = n_puttable_for(side), [2..9] = mask_count(side, region mask a..h). */
 int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream);
+
+/* Linear evaluation from side[i]'s view: out[i] = sum_j W[k][j] * counts()[1+j],
+ * k = learner shard of counts()[0] (see OTH_EVAL_WEIGHTS) -- the model
+ * ProgressPositionMovesLearn.fit_parameter fits (progress_position_moves_learn.py:160-184;
+ * its intercept is not stored, so none is added).  weights: HOST pointer,
+ * OTH_EVAL_WEIGHTS int8, copied into the launch. */
+int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
+             void* stream);
 
 #ifdef __cplusplus
 }

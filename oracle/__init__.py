@@ -34,16 +34,17 @@ def lib():
         L.oracle_legal.argtypes = [P, P, P, I64]
         L.oracle_step.argtypes = [P, P, P, P, P, P, P, P, P, I64]
         L.oracle_result.argtypes = [P, P, P, P, P, I64]
-        L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I]
+        L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I, P]
         L.oracle_sample_midgame.argtypes = [U64, U64, P, P, P, P, I64]
         L.oracle_features.argtypes = [P, P, P, I64]
+        L.oracle_eval.argtypes = [P, P, P, P, I64]
         L.oracle_replay.argtypes = [P, P, P, P, P, P, P, I64]
         L.oracle_game_key.argtypes = [U64, U64]
         L.oracle_game_key.restype = U64
         L.oracle_rng_draws.argtypes = [U64, ctypes.c_uint32]
         L.oracle_rng_draws.restype = ctypes.c_uint32
         for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
-                  "oracle_sample_midgame", "oracle_features", "oracle_replay"):
+                  "oracle_sample_midgame", "oracle_features", "oracle_eval", "oracle_replay"):
             getattr(L, f).restype = I
         _lib = L
     return _lib
@@ -99,8 +100,18 @@ def result(boards):
     return dict(n_black=nb, n_white=nw, diff=d, terminal=t)
 
 
+def _weights(w):
+    w = np.ascontiguousarray(np.asarray(w).reshape(-1))
+    assert w.size == 36 and w.min() >= -128 and w.max() <= 127
+    return w.astype(np.int8)
+
+
 def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=None, record_moves=False,
-            n_threads=0):
+            n_threads=0, weights=None):
+    """policy 0 random, 1 greedy, 2 eval (weights: 36 int8, [shard][feature])."""
+    w = None if weights is None else _weights(weights)
+    if policy == 2 and w is None:
+        raise ValueError("policy 2 (eval) needs weights")
     start = None if start is None else _boards(start)
     st = None if start_turn is None else np.ascontiguousarray(start_turn, np.uint8)
     fb = np.empty((n, 2), np.uint64)
@@ -109,7 +120,7 @@ def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=N
     mv = np.empty((n, MOVES_STRIDE), np.uint8) if record_moves else None
     h = np.zeros(HIST_BINS, np.int64)
     lib().oracle_rollout(_p(start), _p(st), seed, game_id0, policy, n_random, _p(fb), _p(d), _p(pl), _p(mv), _p(h),
-                         n, n_threads)
+                         n, n_threads, _p(w))
     return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h)
 
 
@@ -125,6 +136,14 @@ def features(boards, side):
     side = np.ascontiguousarray(side, np.uint8)
     out = np.empty((len(boards), 10), np.uint8)
     lib().oracle_features(_p(boards), _p(side), _p(out), len(boards))
+    return out
+
+
+def evaluate(boards, side, weights):
+    boards = _boards(boards)
+    side = np.ascontiguousarray(side, np.uint8)
+    out = np.empty(len(boards), np.int32)
+    lib().oracle_eval(_p(boards), _p(side), _p(_weights(weights)), _p(out), len(boards))
     return out
 
 

@@ -253,9 +253,40 @@ int oracle_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, in
     return 0;
 }
 
+/* mask_count, board.py:74-81 */
+static int mask_count(const Board* s, int color, uint64_t mask) {
+    int ret = 0;
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++)
+            if (((mask >> (j + i * 8)) & 1) && s->b[i][j] == color) ret++;
+    return ret;
+}
+
+/* counts(), parameter_progress_position_moves_learn.py:5-17 for side t (1 = 'O', 2 = 'X') */
+static void counts(const Board* s, int t, int o[10]) {
+    static const uint64_t masks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
+                                      0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
+                                      0x0000240000240000ull, 0x0000183C3C180000ull};
+    o[0] = 64 - n_of(s, Empty);
+    o[1] = n_puttable_for(s, t); /* any piece value, as board.py (Empty: hostile = Black) */
+    for (int k = 0; k < 8; k++) o[2 + k] = mask_count(s, t, masks[k]);
+}
+
+/* linear eval of the learner's model: weights row = shard of counts()[0]
+ * (0..16, 17..32, 33..48, 49..64: progress_position_moves_learn.py:112-113),
+ * columns = counts()[1..9] (fit in progress_position_moves_learn.py:160-184) */
+static int eval_of(const Board* s, int t, const int8_t* w) {
+    int o[10];
+    counts(s, t, o);
+    int shard = o[0] <= 16 ? 0 : o[0] <= 32 ? 1 : o[0] <= 48 ? 2 : 3;
+    int v = 0;
+    for (int j = 0; j < 9; j++) v += (int)w[shard * 9 + j] * o[1 + j];
+    return v;
+}
+
 /* One game to terminal from s, game_runner.py:165-201 loop with the build's
  * policies: a side with no move passes ('PS'). */
-static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* moves) {
+static int play_game(Board* s, uint64_t key, int policy, int n_random, const int8_t* w, uint8_t* moves) {
     int ply = 0;
     GameRng rng = rng_init(key);
     while (!is_game_over(s)) {
@@ -265,7 +296,7 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* 
             code = PASS_CODE;
         } else if (policy == 0 || ply < n_random) {
             code = kth_square(legal, rng_pick(&rng, popcount64(legal)));
-        } else {
+        } else if (policy == 1) { /* greedy: minimise the opponent's mobility */
             int best = -1, bestv = 1 << 30;
             for (int sq = 0; sq < 64; sq++) {
                 if (!(legal >> sq & 1)) continue;
@@ -273,6 +304,16 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* 
                 put_code(&c, sq);
                 int v = n_puttable_for(&c, hostile(s->turn));
                 if (v < bestv) { bestv = v; best = sq; }
+            }
+            code = best;
+        } else { /* eval: maximise the mover's linear eval of the child */
+            int best = -1, bestv = -(1 << 30);
+            for (int sq = 0; sq < 64; sq++) {
+                if (!(legal >> sq & 1)) continue;
+                Board c = *s;
+                put_code(&c, sq);
+                int v = eval_of(&c, s->turn, w);
+                if (v > bestv) { bestv = v; best = sq; }
             }
             code = best;
         }
@@ -284,9 +325,11 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, uint8_t* 
     return ply;
 }
 
+/* policy 0 random, 1 greedy, 2 eval (weights: int8[36], used by policy 2 only) */
 int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
-                   int64_t* hist, int64_t n, int n_threads) {
+                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights) {
+    if (policy == 2 && !weights) return -1;
     uint64_t S = seed_state(seed);
     int64_t h[HIST_BINS];
     memset(h, 0, sizeof h);
@@ -303,7 +346,7 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
             if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
             else board_init(&s);
             if (moves) memset(moves + i * MOVES_STRIDE, 255, MOVES_STRIDE);
-            int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random,
+            int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random, weights,
                               moves ? moves + i * MOVES_STRIDE : 0);
             int d = n_of(&s, Black) - n_of(&s, White);
             uint64_t bl, wh;
@@ -360,29 +403,26 @@ int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint
     return 0;
 }
 
-/* mask_count, board.py:74-81 */
-static int mask_count(const Board* s, int color, uint64_t mask) {
-    int ret = 0;
-    for (int i = 0; i < 8; i++)
-        for (int j = 0; j < 8; j++)
-            if (((mask >> (j + i * 8)) & 1) && s->b[i][j] == color) ret++;
-    return ret;
-}
-
 /* counts(), parameter_progress_position_moves_learn.py:5-17 (side 1 = 'O', 2 = 'X') */
 int oracle_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n) {
-    static const uint64_t masks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
-                                      0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
-                                      0x0000240000240000ull, 0x0000183C3C180000ull};
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; i++) {
         Board s;
         board_from_bits(&s, boards[2 * i], boards[2 * i + 1], side[i]);
-        int t = side[i];
-        uint8_t* o = out + i * 10;
-        o[0] = (uint8_t)(64 - n_of(&s, Empty));
-        o[1] = (uint8_t)((t == Black || t == White) ? n_puttable_for(&s, t) : 0);
-        for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)mask_count(&s, t, masks[k]);
+        int o[10];
+        counts(&s, side[i], o);
+        for (int k = 0; k < 10; k++) out[i * 10 + k] = (uint8_t)o[k];
+    }
+    return 0;
+}
+
+/* the learner's linear eval from side[i]'s view (eval_of) */
+int oracle_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        board_from_bits(&s, boards[2 * i], boards[2 * i + 1], side[i]);
+        out[i] = eval_of(&s, side[i], weights);
     }
     return 0;
 }

@@ -101,7 +101,8 @@ struct Position {
     PairProp v, d9, d7;  // the horizontal pair needs no propagators (carry tricks)
     u64 Oi, rOi;          // inner opponent discs, and bit-reversed
     u64 A[8];
-    u64 legal;  // Board.puttables as a mask (board.py:46-52)
+    u64 reach;  // squares one step beyond an attached run (any content)
+    u64 legal;  // Board.puttables as a mask (board.py:46-52) = reach & empty
 };
 
 __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
@@ -129,6 +130,7 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     m = or3(m, sh<8, false>(s.A[3]), sh<9, true>(s.A[4]));
     m = or3(m, sh<9, false>(s.A[5]), sh<7, true>(s.A[6]));
     m |= sh<7, false>(s.A[7]);
+    s.reach = m;
     s.legal = andn(m, P | O);
 }
 
@@ -204,6 +206,17 @@ __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;
     analyse(P, O, s);
     return s.legal;
+}
+
+// Board.puttables(Empty) (board.py:46-52 with piece = Empty, hostile(Empty) =
+// Black, 155-159): empty squares from which a run of >= 1 black disc ends on an
+// empty square -- the mobility counts() reports for a side string other than
+// 'O'/'X' (turn_from_string -> Empty, board.py:245-251).
+__device__ __forceinline__ u64 moves_empty_side(u64 black, u64 white) {
+    const u64 E = ~(black | white);
+    Position s;
+    analyse(E, black, s);
+    return s.reach & E;
 }
 
 // flips of `mv` for mover P with a bracket test per direction (used where the run

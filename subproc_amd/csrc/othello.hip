@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <mutex>
 
@@ -73,6 +74,56 @@ __device__ __forceinline__ u32 greedy_move(const Position& s, u64 P, u64 O, cons
         const u64 f = flips_rays(sq, mv, s, rays);
         const u32 v = (u32)__popcll(moves(andn(O, f), P | f | mv));
         if (v < bestv) {
+            bestv = v;
+            best = sq;
+        }
+    }
+    return best;
+}
+
+// counts() region masks a..h (parameter_progress_position_moves_learn.py:9-16)
+__constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
+                                    0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
+                                    0x0000240000240000ull, 0x0000183C3C180000ull};
+
+// Linear eval (§8f row 2).  Weights: int8 [4][9] (include/othello.h), held as
+// int32 rows padded to 12 in LDS / registers.  The shard of a disc count d is
+// (d - 1) >> 4 for d in 1..64 (shards 0..16, 17..32, 33..48, 49..64 of
+// progress_position_moves_learn.py:112-113).
+constexpr int kEvalRow = 12;
+struct EvalWeights {
+    int8_t w[OTH_EVAL_WEIGHTS];
+};
+__device__ __forceinline__ u32 eval_shard(u32 discs) { return discs ? (min(discs, 64u) - 1u) >> 4 : 0u; }
+__device__ __forceinline__ void eval_weights_to_lds(const EvalWeights& ew, int* w_s) {
+    for (int e = threadIdx.x; e < OTH_EVAL_PHASES * kEvalRow; e += blockDim.x) {
+        const int r = e / kEvalRow, c = e % kEvalRow;
+        w_s[e] = c < OTH_EVAL_FEATURES ? (int)ew.w[r * OTH_EVAL_FEATURES + c] : 0;
+    }
+}
+// sum_j w[j] * counts()[1+j] for the side owning `mine`, with mobility `mob`
+__device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
+    int v = w[0] * (int)__popcll(mob);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v += w[1 + k] * (int)__popcll(mine & kRegionMasks[k]);
+    return v;
+}
+
+// 1-ply eval policy: legal move maximising the mover's eval of the child,
+// ties -> lowest square.  `w` = the weight row of the children's shard (every
+// child has popcount(P|O) + 1 discs).
+__device__ __forceinline__ u32 eval_move(const Position& s, u64 P, u64 O, const u64* rays, const int* w) {
+    u32 best = 64;
+    int bestv = INT_MIN;
+    u64 legal = s.legal;
+    while (legal) {
+        const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
+        const u64 mv = 1ull << sq;
+        legal &= legal - 1;
+        const u64 f = flips_rays(sq, mv, s, rays);
+        const u64 P2 = P | f | mv, O2 = andn(O, f);
+        const int v = eval_linear(w, P2, moves(P2, O2));
+        if (v > bestv) {
             bestv = v;
             best = sq;
         }
@@ -197,6 +248,7 @@ struct RolloutArgs {
     long long* hist;
     int64_t n;
     unsigned long long* work;  // batch counter, zeroed before the launch
+    EvalWeights ew;            // OTH_POLICY_EVAL only
 };
 
 #ifdef OTH_DIAG
@@ -213,9 +265,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
     __shared__ u64 rays[kRayRows * 64];
+    __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? OTH_EVAL_PHASES * kEvalRow : 1];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
+    if (POLICY == OTH_POLICY_EVAL) eval_weights_to_lds(a.ew, w_s);
     __syncthreads();
 
     const int lane = lane_id();
@@ -290,6 +344,12 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs a) {
             u32 sq;
             if (POLICY == OTH_POLICY_GREEDY && (int)ply >= a.n_random) {
                 sq = greedy_move(pos, P, O, rays);
+            } else if (POLICY == OTH_POLICY_EVAL && (int)ply >= a.n_random) {
+                const int* row = w_s + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
+                int w[OTH_EVAL_FEATURES];
+#pragma unroll
+                for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
+                sq = eval_move(pos, P, O, rays, w);
             } else {
                 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
             }
@@ -462,23 +522,52 @@ __global__ __launch_bounds__(kBlock) void book_text_kernel(const u64* __restrict
 // §8f row 2: learner features, counts() of parameter_progress_position_moves_learn.py:5-17:
 // (64 - n_empty, n_puttable_for(side), mask_count(side, m) for the 8 region masks)
 // ---------------------------------------------------------------------------
-__constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
-                                    0x2400810000810024ull, 0x1800008181000018ull, 0x003C424242423C00ull,
-                                    0x0000240000240000ull, 0x0000183C3C180000ull};
+// counts()' view of a board for a side code: 1/2 = 'O'/'X'; 0 = any other
+// side string (turn_from_string -> Empty: mask_count counts empty squares and
+// the mobility is puttables(Empty)); >= 3 has no reference string and matches
+// nothing (mask counts 0, mobility 0, as board.py would for that piece value)
+__device__ __forceinline__ void side_view(ulonglong2 b, u32 sd, u64& mine, u64& mob) {
+    if (sd == OTH_BLACK || sd == OTH_WHITE) {
+        mine = sd == OTH_BLACK ? b.x : b.y;
+        mob = moves_of(mine, sd == OTH_BLACK ? b.y : b.x);
+    } else if (sd == 0) {
+        mine = ~(b.x | b.y);
+        mob = moves_empty_side(b.x, b.y);
+    } else {
+        mine = 0;
+        mob = 0;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void features_kernel(const u64* __restrict__ boards,
                                                           const uint8_t* __restrict__ side,
                                                           uint8_t* __restrict__ out, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards)[i];
-    const u32 sd = side[i];
-    const u64 mine = sd == OTH_BLACK ? b.x : (sd == OTH_WHITE ? b.y : ~(b.x | b.y));
-    const u64 theirs = sd == OTH_BLACK ? b.y : b.x;
+    u64 mine, mob;
+    side_view(b, side[i], mine, mob);
     uint8_t* o = out + i * OTH_FEATURES;
     o[0] = (uint8_t)__popcll(b.x | b.y);
-    o[1] = (uint8_t)((sd == OTH_BLACK || sd == OTH_WHITE) ? __popcll(moves_of(mine, theirs)) : 0);
+    o[1] = (uint8_t)__popcll(mob);
 #pragma unroll
     for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)__popcll(mine & kRegionMasks[k]);
+}
+
+// oth_eval: the linear eval of each position from side[i]'s view (features as
+// features_kernel, side codes as side_view)
+__global__ __launch_bounds__(kBlock) void eval_kernel(const u64* __restrict__ boards, const uint8_t* __restrict__ side,
+                                                      EvalWeights ew, int32_t* __restrict__ out, int64_t n) {
+    __shared__ int w_s[OTH_EVAL_PHASES * kEvalRow];
+    eval_weights_to_lds(ew, w_s);
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards)[i];
+    u64 mine, mob;
+    side_view(b, side[i], mine, mob);
+    const int* w = w_s + kEvalRow * eval_shard((u32)__popcll(b.x | b.y));
+    out[i] = eval_linear(w, mine, mob);
 }
 
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
@@ -487,7 +576,7 @@ inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
 // the calling thread's current device).  Env overrides are tuning knobs for
 // tools/diag only: OTH_ROLLOUT_BLOCKS_PER_CU.
 struct Tuning {
-    unsigned resident_blocks[2];  // per policy
+    unsigned resident_blocks[3];  // per policy
 };
 std::atomic<unsigned long long> g_slot{0};
 
@@ -517,9 +606,10 @@ const DeviceState* device_state() {
     if (!d.ready.load(std::memory_order_relaxed)) {
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const void* kern[2] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM, false>),
-                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY, false>)};
-        for (int p = 0; p < 2; p++) {
+        const void* kern[3] = {reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_RANDOM, false>),
+                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_GREEDY, false>),
+                               reinterpret_cast<const void*>(rollout_kernel<OTH_POLICY_EVAL, false>)};
+        for (int p = 0; p < 3; p++) {
             int per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
             // 5 blocks of 4 waves per CU (5 waves/SIMD) measured fastest for the
@@ -580,11 +670,10 @@ int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_
     return launched();
 }
 
-int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
-                int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist,
-                int64_t n, void* stream) {
-    if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
-    if (n == 0) return OTH_OK;
+namespace {
+int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                   int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                   uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
     RolloutArgs a;
     a.start = start;
     a.start_turn = start_turn;
@@ -598,6 +687,7 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     a.moves = moves;
     a.hist = (long long*)hist;
     a.n = n;
+    for (int k = 0; k < OTH_EVAL_WEIGHTS; k++) a.ew.w[k] = weights ? weights[k] : 0;
     const DeviceState* ds = device_state();
     if (!ds) return status(hipErrorInvalidDevice);
     const Tuning& t = ds->tuning;
@@ -608,7 +698,10 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
     hipStream_t st = (hipStream_t)stream;
-    if (policy == OTH_POLICY_GREEDY) {
+    if (policy == OTH_POLICY_EVAL) {
+        if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
+        else rollout_kernel<OTH_POLICY_EVAL, false><<<grid, kBlock, 0, st>>>(a);
+    } else if (policy == OTH_POLICY_GREEDY) {
         if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_GREEDY, false><<<grid, kBlock, 0, st>>>(a);
     } else {
@@ -616,6 +709,25 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
     return launched();
+}
+}  // namespace
+
+int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist,
+                int64_t n, void* stream) {
+    if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return rollout_launch(start, start_turn, seed, game_id0, policy, n_random, nullptr, final_boards, diff, plies,
+                          moves, hist, n, stream);
+}
+
+int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                     int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                     uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+    if (n < 0 || !weights) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights, final_boards, diff,
+                          plies, moves, hist, n, stream);
 }
 
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
@@ -640,6 +752,16 @@ int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int6
     if (n < 0 || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     features_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards, side, out, n);
+    return launched();
+}
+
+int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
+             void* stream) {
+    if (n < 0 || !weights || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    EvalWeights ew;
+    for (int k = 0; k < OTH_EVAL_WEIGHTS; k++) ew.w[k] = weights[k];
+    eval_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards, side, ew, out, n);
     return launched();
 }
 

@@ -13,15 +13,18 @@ Reference mapping (board.py line numbers):
   step    -> Board.put_s / put         161-209
   result  -> n_black / n_white / is_game_over 37-58 + game_runner.py:194-199
   rollout -> GameRunner.play_a_game loop   game_runner.py:165-201
+  evaluate -> linear eval of the learner's counts() features
 """
+import ctypes
 from collections import namedtuple
 
 import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BLACK, BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, PASS, POLICY_GREEDY, POLICY_RANDOM,
-                   POS_STRIDE, WHITE, check)
+from ._lib import (BLACK, BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, PASS, POLICY_EVAL, POLICY_GREEDY,
+                   POLICY_RANDOM, POS_STRIDE, WHITE, check)
+from .params import DEFAULT_WEIGHTS, as_weights
 
 StepResult = namedtuple("StepResult", "boards turn flips legal_next ret")
 Result = namedtuple("Result", "n_black n_white diff terminal")
@@ -29,8 +32,14 @@ RolloutResult = namedtuple("RolloutResult", "final_boards diff plies moves hist"
 Positions = namedtuple("Positions", "boards turn nturn move")
 Replay = namedtuple("Replay", "boards turn end")
 
-_POLICIES = {"random": POLICY_RANDOM, "greedy": POLICY_GREEDY, POLICY_RANDOM: POLICY_RANDOM,
-             POLICY_GREEDY: POLICY_GREEDY}
+_POLICIES = {"random": POLICY_RANDOM, "greedy": POLICY_GREEDY, "eval": POLICY_EVAL, POLICY_RANDOM: POLICY_RANDOM,
+             POLICY_GREEDY: POLICY_GREEDY, POLICY_EVAL: POLICY_EVAL}
+
+
+def _weights_ptr(weights):
+    """Host int8[36] buffer for oth_eval / oth_rollout_eval (copied into the launch)."""
+    w = as_weights(DEFAULT_WEIGHTS if weights is None else weights)
+    return (ctypes.c_int8 * w.size).from_buffer_copy(w.tobytes())
 
 
 def _stream():
@@ -139,7 +148,7 @@ def result(boards):
 
 
 def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start_turn=None, record_moves=False,
-            hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True):
+            hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True, weights=None):
     """Play n games to terminal on the GPU (one lane per game).
 
     Game i uses the RNG stream of global id game_id0 + i, so results do not
@@ -147,9 +156,13 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     is accumulated into if given (zero it yourself), else a fresh zeroed one is
     returned: [0..128] diff+64, 129 black wins, 130 white wins, 131 draws,
     132 total plies (= env-steps).
+
+    Policies: "random"; "greedy" (minimise the opponent's mobility) and "eval"
+    (maximise the mover's linear eval under ``weights``, int8 [4, 9], default
+    params.DEFAULT_WEIGHTS) after ``n_random`` random plies.
     """
     if policy not in _POLICIES:
-        raise ValueError(f"policy must be 'random' or 'greedy', got {policy!r}")
+        raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
     d = _device(device) if start is None else start.device
     ps = pst = None
     if start is not None:
@@ -169,8 +182,15 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
         return None if t is None else t.data_ptr()
 
     with torch.cuda.device(d):
-        check(_lib.load().oth_rollout(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy], n_random, ptr(fb),
-                                      ptr(df), ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout")
+        if _POLICIES[policy] == POLICY_EVAL:
+            check(_lib.load().oth_rollout_eval(ps, pst, seed & (2**64 - 1), game_id0, n_random, _weights_ptr(weights),
+                                               ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()),
+                  "oth_rollout_eval")
+        else:
+            if weights is not None:
+                raise ValueError("weights apply to policy 'eval' only")
+            check(_lib.load().oth_rollout(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy], n_random,
+                                          ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout")
     return RolloutResult(fb, df, pl, mv, hist)
 
 
@@ -229,6 +249,19 @@ def features(boards, side):
     out = torch.empty((n, N_FEATURES), dtype=torch.uint8, device=boards.device)
     with torch.cuda.device(boards.device):
         check(_lib.load().oth_features(pb, ps, out.data_ptr(), n, _stream()), "oth_features")
+    return out
+
+
+def evaluate(boards, side, weights=None):
+    """Linear eval of each position from side 1 ('O') / 2 ('X')'s view: int32
+    (n,) = sum_j W[shard(discs)][j] * counts()[1+j] (include/othello.h oth_eval;
+    the model progress_position_moves_learn.py:160-184 fits)."""
+    n = _n(boards)
+    pb = _dev(boards, "boards", torch.int64)
+    ps = _dev(side, "side", torch.uint8, (n,))
+    out = torch.empty(n, dtype=torch.int32, device=boards.device)
+    with torch.cuda.device(boards.device):
+        check(_lib.load().oth_eval(pb, ps, _weights_ptr(weights), out.data_ptr(), n, _stream()), "oth_eval")
     return out
 
 

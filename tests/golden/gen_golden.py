@@ -56,10 +56,11 @@ RB = load_reference_board()
 Board = RB["Board"]
 
 
-def load_reference_counts():
+def load_reference_counts(want_ns=False):
     """parameter_progress_position_moves_learn.counts (and parameter.board_from_a_book)
     from the reference, exec'd against the shimmed board module.  Both files are
-    valid Python 3 as they stand; nothing is copied."""
+    valid Python 3 as they stand; nothing is copied.  want_ns=True returns the
+    module namespace (for ProgressPositionMovesParameter.default_value)."""
     import types
     mod_board = types.ModuleType("board")
     mod_board.__dict__.update(RB)
@@ -73,7 +74,7 @@ def load_reference_counts():
         ns = {"__name__": "reference_ppml"}
         exec(compile(open("/root/reference/parameter_progress_position_moves_learn.py").read(),
                      "reference_ppml.py", "exec"), ns)
-        return ns["counts"]
+        return ns if want_ns else ns["counts"]
     finally:
         for k, v in saved.items():
             if v is None:
@@ -188,9 +189,13 @@ def play(args):
     policy 0 = random (k-th legal square, LSB-first == puttables order);
     policy 1 = greedy: for ply >= n_random pick the legal move minimising the
     opponent's n_puttable_for on the child, ties -> first in puttables order.
+    policy 2 = eval: for ply >= n_random pick the legal move maximising the
+    mover's linear eval of the child (eval_value: the reference's own counts()
+    on the child's book record), ties -> first in puttables order.
     A side with no legal move passes ('ps'), as the engines do in game_runner.
     """
-    seed, g, policy, n_random, bl, wh, turn = args
+    seed, g, policy, n_random, bl, wh, turn = args[:7]
+    weights = args[7] if len(args) > 7 else None
     rng = GameRng(game_key(seed_state(seed), g))
     b = from_bits(bl, wh, turn)
     moves = []
@@ -202,7 +207,7 @@ def play(args):
         elif policy == 0 or ply < n_random:
             x, y = puts[rng.pick(len(puts))]
             code = x + 8 * y
-        else:
+        elif policy == 1:
             best, bestv = None, None
             for (x, y) in puts:
                 c = clone(b)
@@ -211,12 +216,39 @@ def play(args):
                 if bestv is None or v < bestv:
                     best, bestv = x + 8 * y, v
             code = best
+        else:
+            best, bestv = None, None
+            for (x, y) in puts:
+                c = clone(b)
+                assert c.put_s(c.handstr_from_coord(x, y)) > 0
+                v = eval_value(c, "O" if b.turn == Black else "X", weights)
+                if bestv is None or v > bestv:
+                    best, bestv = x + 8 * y, v
+            code = best
         r = b.put_s(code_to_str(b, code))
         assert r >= 0
         moves.append(code)
         ply += 1
     fb, fw = to_bits(b)
     return moves, fb, fw, b.n_black() - b.n_white(), ply
+
+
+# learner shards of the disc count (ProgressPositionMovesLearn.__get_fit_parameters_shards,
+# progress_position_moves_learn.py:112-113; that module needs pyres/slack, so the
+# four bounds are restated here)
+EVAL_SHARDS = ((0, 16), (17, 32), (33, 48), (49, 64))
+_COUNTS = None
+
+
+def eval_value(b, side, weights):
+    """The learner's linear model on a board: sum_j W[shard(counts[0])][j] * counts[1+j]
+    with the reference's counts() (fit in progress_position_moves_learn.py:160-184)."""
+    global _COUNTS
+    if _COUNTS is None:
+        _COUNTS = load_reference_counts()
+    f = _COUNTS({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn}, side)
+    k = [i for i, (lo, hi) in enumerate(EVAL_SHARDS) if lo <= f[0] <= hi][0]
+    return sum(int(weights[k][j]) * int(f[1 + j]) for j in range(9))
 
 
 def sample_midgame(args):
@@ -374,10 +406,10 @@ def main():
     )
 
     # ---------------------------------------------------------------- rollouts
-    def rollouts(name, seed, g0, n, policy, n_random, starts=None):
+    def rollouts(name, seed, g0, n, policy, n_random, starts=None, weights=None):
         if starts is None:
             starts = [(ib, iw, Black)] * n
-        args = [(seed, g0 + i, policy, n_random, s[0], s[1], s[2]) for i, s in enumerate(starts)]
+        args = [(seed, g0 + i, policy, n_random, s[0], s[1], s[2], weights) for i, s in enumerate(starts)]
         res = pool.map(play, args, chunksize=4)
         mv = np.full((n, 128), 255, np.uint8)
         for i, r in enumerate(res):
@@ -389,7 +421,8 @@ def main():
             start_black=u64([s[0] for s in starts]), start_white=u64([s[1] for s in starts]),
             start_turn=np.array([s[2] for s in starts], np.uint8),
             moves=mv, final_black=u64([r[1] for r in res]), final_white=u64([r[2] for r in res]),
-            diff=np.array([r[3] for r in res], np.int8), plies=np.array([r[4] for r in res], np.uint8))
+            diff=np.array([r[3] for r in res], np.int8), plies=np.array([r[4] for r in res], np.uint8),
+            **({} if weights is None else {"weights": np.array(weights, np.int8)}))
 
     rollouts("rollout_random", SEED, 0, 256, 0, 0)
     rollouts("rollout_random_offset", 12345, (1 << 20) * 3 + 77, 128, 0, 0)
@@ -397,6 +430,23 @@ def main():
     rollouts("rollout_random_from_mid", 777, 5, len(mid), 0, 0, starts=mid)
     rollouts("rollout_greedy", SEED, 0, 192, 1, 10)
     rollouts("rollout_greedy_from_mid", 99, 1000, 64, 1, 0, starts=mid[:64])
+
+    # ---------------------------------------------------------------- eval policy + linear eval (§8f row 2)
+    ns = load_reference_counts(want_ns=True)
+    wdef = [list(r) for r in ns["ProgressPositionMovesParameter"]().default_value()]
+    wrand = np.random.default_rng(77).integers(-127, 128, (4, 9)).tolist()
+    rollouts("rollout_eval", SEED, 0, 128, 2, 10, weights=wdef)
+    rollouts("rollout_eval_rand_from_mid", 4242, 77, 64, 2, 0, starts=mid[:64], weights=wrand)
+    boards = [from_bits(p[0], p[1], p[2]) for p in pos[:512]]
+    np.savez_compressed(
+        os.path.join(OUT, "eval_values.npz"),
+        black=u64([p[0] for p in pos[:512]]), white=u64([p[1] for p in pos[:512]]),
+        weights_default=np.array(wdef, np.int8), weights_rand=np.array(wrand, np.int8),
+        # columns: side 'O', 'X', '-' (any other string: turn_from_string -> Empty)
+        counts=np.array([[list(ns["counts"]({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn},
+                                      sd)) for sd in ("O", "X", "-")] for b in boards], np.uint8),
+        eval_default=np.array([[eval_value(b, sd, wdef) for sd in ("O", "X", "-")] for b in boards], np.int32),
+        eval_rand=np.array([[eval_value(b, sd, wrand) for sd in ("O", "X", "-")] for b in boards], np.int32))
 
     # ---------------------------------------------------------------- config-2 generator
     sm = pool.map(sample_midgame, [(SEED, i) for i in range(256)], chunksize=4)

@@ -108,9 +108,8 @@ def test_inplace_step_aliasing():
 
 @pytest.mark.parametrize("n,off", [(1, 0), (3, 0), (4, 0), (4093, 0), (4096, 1), (4097, 3), (1023, 2)])
 def test_step_ragged_and_unaligned(n, off):
-    """The step kernel packs 4 boards per thread for aligned arrays (n % 4 tail
-    per board) and runs unaligned views (offset byte arrays) per board: both
-    paths against the oracle, including the uint8 nturn wrap at 255."""
+    """Ragged sizes and offset views (byte arrays at odd addresses) against the
+    oracle, including the uint8 nturn wrap at 255."""
     rng = np.random.default_rng(n + off)
     m = n + off
     occ = rng.integers(0, 2**64, m, dtype=np.uint64) & rng.integers(0, 2**64, m, dtype=np.uint64)
@@ -147,10 +146,11 @@ def test_rollout_fixtures(name):
     z = load_npz(name + ".npz")
     n = len(z["plies"])
     from_mid = "from_mid" in name
-    policy = "greedy" if int(z["policy"]) == 1 else "random"
+    policy = {0: "random", 1: "greedy", 2: "eval"}[int(z["policy"])]
     r = ops.rollout(n, int(z["seed"]), int(z["game_id0"]), policy, int(z["n_random"]),
                     start=B(z["start_black"], z["start_white"]) if from_mid else None,
-                    start_turn=T(z["start_turn"]) if from_mid else None, record_moves=True, device=DEV)
+                    start_turn=T(z["start_turn"]) if from_mid else None, record_moves=True, device=DEV,
+                    weights=z.get("weights"))
     np.testing.assert_array_equal(r.moves.cpu().numpy(), z["moves"])
     np.testing.assert_array_equal(r.plies.cpu().numpy(), z["plies"])
     np.testing.assert_array_equal(r.diff.cpu().numpy(), z["diff"])
@@ -233,13 +233,55 @@ def test_rollout_greedy_4096_vs_oracle():
     assert (r.hist.cpu().numpy() == o["hist"]).all()
 
 
+def test_rollout_eval_4096_vs_oracle():
+    from subproc_amd.params import DEFAULT_WEIGHTS
+    n = 4096
+    for w in (DEFAULT_WEIGHTS, np.random.default_rng(5).integers(-127, 128, (4, 9)).astype(np.int8)):
+        r = ops.rollout(n, 43, 1 << 21, "eval", 10, weights=w, device=DEV)
+        o = oracle.rollout(n, 43, 1 << 21, policy=2, n_random=10, weights=w)
+        assert (U(r.final_boards) == o["final_boards"]).all()
+        assert (r.plies.cpu().numpy() == o["plies"]).all()
+        assert (r.hist.cpu().numpy() == o["hist"]).all()
+
+
+def test_eval_values():
+    z = load_npz("eval_values.npz")
+    boards = B(z["black"], z["white"])
+    n = len(z["black"])
+    for col, side in ((0, 1), (1, 2), (2, 0)):  # 'O', 'X', '-' (turn_from_string -> Empty)
+        sides = T(np.full(n, side))
+        np.testing.assert_array_equal(ops.features(boards, sides).cpu().numpy(), z["counts"][:, col])
+        for wk, ek in (("weights_default", "eval_default"), ("weights_rand", "eval_rand")):
+            got = ops.evaluate(boards, sides, z[wk])
+            np.testing.assert_array_equal(got.cpu().numpy(), z[ek][:, col])
+
+
+def test_eval_random_boards_vs_oracle():
+    """Arbitrary disjoint boards (every disc count), all three side codes."""
+    rng = np.random.default_rng(9)
+    n = 32768
+    occ = rng.integers(0, 2**64, n, dtype=np.uint64) & rng.integers(0, 2**64, n, dtype=np.uint64)
+    occ[: n // 4] = rng.integers(0, 2**64, n // 4, dtype=np.uint64)  # dense boards
+    col = rng.integers(0, 2**64, n, dtype=np.uint64)
+    nb = np.stack([occ & col, occ & ~col], 1)
+    w = rng.integers(-128, 128, (4, 9)).astype(np.int8)
+    side = rng.integers(0, 4, n).astype(np.uint8)
+    got = ops.evaluate(B(nb[:, 0], nb[:, 1]), T(side), w).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.evaluate(nb, side, w))
+    feats = ops.features(B(nb[:, 0], nb[:, 1]), T(side)).cpu().numpy()
+    np.testing.assert_array_equal(feats, oracle.features(nb, side))
+
+
 def test_rollout_from_start_positions_vs_oracle():
+    from subproc_amd.params import DEFAULT_WEIGHTS
     n = 16384
     p = ops.sample_midgame(n, 11, device=DEV)
-    for policy, pid in (("random", 0), ("greedy", 1)):
-        r = ops.rollout(n, 5, 77, policy, 0, start=p.boards, start_turn=p.turn, record_moves=True, device=DEV)
+    for policy, pid in (("random", 0), ("greedy", 1), ("eval", 2)):
+        w = DEFAULT_WEIGHTS if pid == 2 else None
+        r = ops.rollout(n, 5, 77, policy, 0, start=p.boards, start_turn=p.turn, record_moves=True, device=DEV,
+                        weights=w)
         o = oracle.rollout(n, 5, 77, pid, 0, start=U(p.boards), start_turn=p.turn.cpu().numpy(),
-                           record_moves=True)
+                           record_moves=True, weights=w)
         assert (r.moves.cpu().numpy() == o["moves"]).all(), policy
         assert (U(r.final_boards) == o["final_boards"]).all(), policy
         assert (r.hist.cpu().numpy() == o["hist"]).all(), policy

@@ -75,7 +75,8 @@ def test_rollouts(name):
     from_mid = "from_mid" in name
     r = oracle.rollout(n, int(z["seed"]), int(z["game_id0"]), int(z["policy"]), int(z["n_random"]),
                        start=np.stack([z["start_black"], z["start_white"]], 1) if from_mid else None,
-                       start_turn=z["start_turn"] if from_mid else None, record_moves=True)
+                       start_turn=z["start_turn"] if from_mid else None, record_moves=True,
+                       weights=z.get("weights"))
     np.testing.assert_array_equal(r["moves"], z["moves"])
     np.testing.assert_array_equal(r["plies"], z["plies"])
     np.testing.assert_array_equal(r["diff"], z["diff"])
@@ -84,6 +85,22 @@ def test_rollouts(name):
     hist = r["hist"]
     assert hist[:129].sum() == n and hist[129:132].sum() == n and hist[132] == int(z["plies"].sum())
     np.testing.assert_array_equal(hist[:129], np.bincount(z["diff"].astype(np.int64) + 64, minlength=129))
+
+
+def test_eval_values():
+    """oracle_eval against the reference's counts() + the learner's linear model
+    (eval_values.npz: default_value() weights and a random int8 table)."""
+    z = load_npz("eval_values.npz")
+    boards = np.stack([z["black"], z["white"]], 1)
+    n = len(boards)
+    for col, side in ((0, 1), (1, 2), (2, 0)):  # 'O', 'X', '-' (turn_from_string -> Empty)
+        sides = np.full(n, side, np.uint8)
+        np.testing.assert_array_equal(oracle.features(boards, sides), z["counts"][:, col])
+        for wk, ek in (("weights_default", "eval_default"), ("weights_rand", "eval_rand")):
+            np.testing.assert_array_equal(oracle.evaluate(boards, sides, z[wk]), z[ek][:, col])
+    # every learner shard is exercised
+    discs = np.array([bin(int(b) | int(w)).count("1") for b, w in boards])
+    assert len({0 if d <= 16 else 1 if d <= 32 else 2 if d <= 48 else 3 for d in discs}) == 4
 
 
 def test_sample_midgame():

@@ -12,6 +12,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
+CPU_ABI_PATH = os.path.join(_HERE, "libothello_cpu.so")
 HIST_BINS = 133
 MOVES_STRIDE = 128
 
@@ -19,8 +20,28 @@ _lib = None
 
 
 def build(force=False):
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    if force or not os.path.exists(LIB_PATH) or not os.path.exists(CPU_ABI_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "all"])
+
+
+_cpu_abi = None
+
+
+def cpu_abi():
+    """libothello_cpu.so: include/othello.h on host memory, bound
+    with the product's own signature table so both libraries are called alike."""
+    global _cpu_abi
+    if _cpu_abi is None:
+        from subproc_amd._lib import SIGNATURES  # the table only; loads no GPU code
+        if not os.path.exists(CPU_ABI_PATH):
+            build()
+        L = ctypes.CDLL(CPU_ABI_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _cpu_abi = L
+    return _cpu_abi
 
 
 def lib():

@@ -1,0 +1,127 @@
+/*
+ * othello_cpu_abi.c — libothello_cpu.so: the C-ABI of include/othello.h built
+ * for the HOST on top of the parity oracle (othello_oracle.c).
+ *
+ * TEST INFRASTRUCTURE ONLY.  SURVEY.md §8(b)/(c) ask for a CPU build of the
+ * same header that gives identical results, so parity can be checked at the
+ * ABI itself: tests call the same entry points with the same arguments on this
+ * library (host pointers) and on libsubproc_amd_hip.so (device pointers) and
+ * compare.  The product package never loads this library.
+ *
+ * Differences from the HIP library, by design:
+ *   - every pointer is HOST memory; `stream` is ignored (calls are synchronous);
+ *   - OpenMP over all host threads where the oracle parallelises.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/othello.h"
+
+/* the oracle's exported functions (othello_oracle.c) */
+int oracle_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n);
+int oracle_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int64_t n);
+int oracle_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* move, uint64_t* boards_out,
+                uint8_t* turn_out, uint64_t* flips, uint64_t* legal_next, int8_t* ret, uint8_t* nturn, int64_t n);
+int oracle_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff, uint8_t* terminal,
+                  int64_t n);
+int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                   int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
+                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights);
+int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
+                          uint8_t* move, int64_t n);
+int oracle_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n);
+int oracle_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n);
+int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+                  uint64_t* pos, uint8_t* pos_turn, uint8_t* pos_end, int64_t n);
+
+const char* oth_version(void) { return "subproc_amd-cpu 0.1.0 host (oracle)"; }
+
+int oth_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && !boards)) return OTH_EINVAL;
+    return oracle_reset(boards, turn, nturn, n);
+}
+
+int oth_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!boards || !turn || !legal))) return OTH_EINVAL;
+    return oracle_legal(boards, turn, legal, n);
+}
+
+int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* move, uint64_t* boards_out,
+             uint8_t* turn_out, uint64_t* flips, uint64_t* legal_next, int8_t* ret, uint8_t* nturn, int64_t n,
+             void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!boards_in || !turn_in || !move))) return OTH_EINVAL;
+    return oracle_step(boards_in, turn_in, move, boards_out, turn_out, flips, legal_next, ret, nturn, n);
+}
+
+int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff, uint8_t* terminal,
+               int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && !boards)) return OTH_EINVAL;
+    return oracle_result(boards, n_black, n_white, diff, terminal, n);
+}
+
+int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist,
+                int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return oracle_rollout(start, start_turn, seed, game_id0, policy, n_random, final_boards, diff, plies, moves, hist,
+                          n, 0, NULL);
+}
+
+int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                     int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                     uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || !weights) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return oracle_rollout(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, final_boards, diff, plies,
+                          moves, hist, n, 0, weights);
+}
+
+int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
+                       uint8_t* move, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!boards || !turn || !move))) return OTH_EINVAL;
+    return oracle_sample_midgame(seed, index0, boards, turn, nturn, move, n);
+}
+
+int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+               uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!moves || !plies || !pos_boards))) return OTH_EINVAL;
+    return oracle_replay(start, start_turn, moves, plies, pos_boards, pos_turn, pos_end, n);
+}
+
+/* serialize_str (board.py:214-243) + '\n': 64 chars row-major, 'O' black,
+ * 'X' white, '-' empty, then ' ' and the side to move ('O', 'X', or '-'). */
+int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!boards || !turn || !out))) return OTH_EINVAL;
+    for (int64_t i = 0; i < n; i++) {
+        char* line = out + i * OTH_BOOK_LINE;
+        const uint64_t bl = boards[2 * i], wh = boards[2 * i + 1];
+        for (int sq = 0; sq < 64; sq++) line[sq] = (bl >> sq & 1) ? 'O' : ((wh >> sq & 1) ? 'X' : '-');
+        line[64] = ' ';
+        line[65] = turn[i] == OTH_BLACK ? 'O' : (turn[i] == OTH_WHITE ? 'X' : '-');
+        line[66] = '\n';
+    }
+    return OTH_OK;
+}
+
+int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
+    return oracle_features(boards, side, out, n);
+}
+
+int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
+             void* stream) {
+    (void)stream;
+    if (n < 0 || !weights || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
+    return oracle_eval(boards, side, weights, out, n);
+}

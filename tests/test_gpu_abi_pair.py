@@ -1,0 +1,115 @@
+"""The same include/othello.h calls on both builds of the header: the HIP library
+(device buffers, raw ctypes, no ops.py wrapper) and libothello_cpu.so (host
+buffers, the oracle restatement).  Outputs must be bit-identical
+(on the GPU box parity is against the fixtures and the build's
+own CPU library)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from subproc_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+HOSTP = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+
+
+class Buf:
+    """One logical buffer held twice: numpy (host library) and torch (device library)."""
+
+    def __init__(self, a):
+        self.h = np.ascontiguousarray(a)
+        dt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint8: torch.uint8, np.int8: torch.int8,
+              np.int32: torch.int32}[self.h.dtype.type]
+        src = self.h.view(np.int64) if self.h.dtype == np.uint64 else self.h
+        self.d = torch.from_numpy(src.copy()).to(dt).to(DEV)
+
+    def device_as_host(self):
+        a = self.d.cpu().numpy()
+        return a.view(np.uint64) if self.h.dtype == np.uint64 else a
+
+
+def both(name, *args):
+    """Call `name` on both libraries; Buf arguments become host / device pointers."""
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    stream = torch.cuda.current_stream().cuda_stream
+    ha = [HOSTP(a.h) if isinstance(a, Buf) else a for a in args]
+    da = [a.d.data_ptr() if isinstance(a, Buf) else a for a in args]
+    assert getattr(cpu, name)(*ha, None) == 0, name
+    assert getattr(gpu, name)(*da, stream) == 0, name
+    torch.cuda.synchronize()
+
+
+def same(*bufs):
+    for b in bufs:
+        np.testing.assert_array_equal(b.device_as_host(), b.h)
+
+
+def positions(n, seed):
+    b, t, nt, m = (Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint8)),
+                   Buf(np.zeros(n, np.uint8)))
+    both("oth_sample_midgame", seed, 0, b, t, nt, m, n)
+    same(b, t, nt, m)
+    return b, t, nt, m
+
+
+def test_step_pair():
+    n = 65536
+    b, t, nt, m = positions(n, 0x5EED)
+    outs = [Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint64)),
+            Buf(np.zeros(n, np.uint64)), Buf(np.zeros(n, np.int8))]
+    both("oth_step", b, t, m, *outs, nt, n)
+    same(*outs, nt)
+    # result + legal on the stepped boards
+    res = [Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.int8)),
+           Buf(np.zeros(n, np.uint8))]
+    both("oth_result", outs[0], *res, n)
+    same(*res)
+    leg = Buf(np.zeros(n, np.uint64))
+    both("oth_legal", outs[0], outs[1], leg, n)
+    same(leg)
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2])
+def test_rollout_pair(policy):
+    n = 8192
+    b, t, _, _ = positions(n, 3)
+    outs = [Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.int8)), Buf(np.zeros(n, np.uint8)),
+            Buf(np.zeros((n, _lib.MOVES_STRIDE), np.uint8)), Buf(np.zeros(_lib.HIST_BINS, np.int64))]
+    if policy == 2:
+        w = (ctypes.c_int8 * 36)(*np.random.default_rng(1).integers(-127, 128, 36).tolist())
+        both("oth_rollout_eval", None, None, 99, 1 << 30, 10, w, *outs, n)
+        both("oth_rollout_eval", b, t, 98, 5, 0, w, *outs, n)  # from mid-game starts, hist accumulates
+    else:
+        both("oth_rollout", None, None, 99, 1 << 30, policy, 10, *outs, n)
+        both("oth_rollout", b, t, 98, 5, policy, 0, *outs, n)
+    same(*outs)
+
+
+def test_books_features_eval_pair():
+    n = 512
+    outs = [None, None, Buf(np.zeros(n, np.uint8)), Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8)), None]
+    both("oth_rollout", None, None, 5, 0, 0, 0, None, None, outs[2], outs[3], None, n)
+    same(outs[2], outs[3])
+    pos = Buf(np.zeros((n, _lib.POS_STRIDE, 2), np.uint64))
+    pt, pe = Buf(np.zeros((n, _lib.POS_STRIDE), np.uint8)), Buf(np.zeros((n, _lib.POS_STRIDE), np.uint8))
+    both("oth_replay", None, None, outs[3], outs[2], pos, pt, pe, n)
+    # rows past plies are left untouched by both (zero-initialised here)
+    same(pos, pt, pe)
+    k = n * _lib.POS_STRIDE
+    flat_b = Buf(pos.h.reshape(k, 2))
+    flat_t = Buf(pt.h.reshape(k))
+    txt = Buf(np.zeros(k * _lib.BOOK_LINE, np.uint8))
+    both("oth_book_text", flat_b, flat_t, k, txt)
+    same(txt)
+    side = Buf(np.random.default_rng(2).integers(0, 4, k).astype(np.uint8))
+    feats = Buf(np.zeros((k, _lib.N_FEATURES), np.uint8))
+    both("oth_features", flat_b, side, feats, k)
+    ev = Buf(np.zeros(k, np.int32))
+    w = (ctypes.c_int8 * 36)(*np.random.default_rng(3).integers(-128, 128, 36).tolist())
+    both("oth_eval", flat_b, side, w, ev, k)
+    same(feats, ev)

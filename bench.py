@@ -15,6 +15,8 @@ Also reported on rank 0 (secondary, same JSON line):
     positions (52 algorithmic HBM bytes per step), repeated launches;
   * step_steady: the same kernel over 16,777,216 positions (HBM roofline);
   * greedy     : config 5, 1,048,576 1-ply greedy-mobility games;
+  * eval       : 1,048,576 games of the 1-ply linear-eval policy with the
+    learner's default weights (SURVEY.md §8f row 2);
   * cpu_baseline: the C oracle (mailbox restatement of board.py) on a bounded
     sample of the same workload on the host cores.
 
@@ -204,6 +206,7 @@ def main():
                                                  lambda x: x, launches=10)
         if args.workload != "greedy":
             sec["greedy_1M"] = _bench_greedy(ops, torch, dev, stream, args)
+        sec["eval_1M"] = _bench_greedy(ops, torch, dev, stream, args, policy="eval")
         out["secondary"] = sec
         out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
     if rank == 0:
@@ -254,17 +257,20 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
     return r
 
 
-def _bench_greedy(ops, torch, dev, stream, args):
+def _bench_greedy(ops, torch, dev, stream, args, policy="greedy"):
+    """config 5 (policy "greedy") or the eval-table policy (§8f row 2, default
+    learner weights): n games, 10 random plies, then the 1-ply policy."""
     n = args.games
     hist = torch.zeros(133, dtype=torch.int64, device=dev)
-    ops.rollout(n // 16, args.seed, 0, "greedy", 10, hist=hist, device=dev, want_boards=False)
+    ops.rollout(n // 16, args.seed, 0, policy, 10, hist=hist, device=dev, want_boards=False)
     torch.cuda.synchronize()
     hist.zero_()
     t0 = time.perf_counter()
-    ops.rollout(n, args.seed, 1 << 40, "greedy", 10, hist=hist, device=dev)
+    ops.rollout(n, args.seed, 1 << 40, policy, 10, hist=hist, device=dev)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"metric": "env-steps/sec (greedy-mobility self-play)", "value": int(hist[132]) / dt,
+    what = "greedy-mobility" if policy == "greedy" else "linear-eval (learner default weights)"
+    return {"metric": f"env-steps/sec ({what} self-play)", "value": int(hist[132]) / dt,
             "unit": "env-steps/s", "games": n, "ms": dt * 1e3}
 
 

@@ -151,10 +151,12 @@ def main():
         drain()
         barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
         t0 = time.perf_counter()
         ev0.record(stream)
-        for s in range(args.warmup, args.warmup + args.steps):
+        for k, s in enumerate(range(args.warmup, args.warmup + args.steps)):
             one_step(s)
+            step_ev[k].record(stream)
         if use_dist and args.allreduce == "end":
             total = hists[args.warmup:].sum(0)
             dist.all_reduce(total, op=dist.ReduceOp.SUM)
@@ -166,6 +168,11 @@ def main():
         t1 = time.perf_counter()
         elapsed = max_over_ranks(t1 - t0)
         kern_ms = ev0.elapsed_time(ev1) / args.steps  # stream-ordered: the rollout launch (+ all-reduce at N>1)
+        # per-step stream time (launch + counter memset), median over the K timed steps
+        per_step = sorted([ev0.elapsed_time(step_ev[0])] +
+                          [step_ev[k - 1].elapsed_time(step_ev[k]) for k in range(1, args.steps)])
+        median_ms = per_step[len(per_step) // 2] if len(per_step) % 2 else \
+            0.5 * (per_step[len(per_step) // 2 - 1] + per_step[len(per_step) // 2])
         timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) when distributed
         env_steps = int(timed[132])
         games = n * world * args.steps
@@ -186,7 +193,8 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": achieved / HBM_PEAK_GBS,
                            "traffic": prof.get("hbm_bytes") if prof else None,
-                           "kernel": kname, "launch_ms": kern_ms, "profile": pfile if prof else None,
+                           "kernel": kname, "launch_ms": kern_ms, "launch_ms_median": median_ms,
+                           "profile": pfile if prof else None,
                            "note": "%d algorithmic B/game written (final board, diff, plies); the kernel is "
                                    "integer-VALU-bound, see 'valu'" % ROLLOUT_BYTES_PER_GAME}
         if prof and "SQ_INSTS_VALU" in prof:

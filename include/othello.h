@@ -152,6 +152,31 @@ int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int6
 int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
              void* stream);
 
+/* TD state map of ProgressPositionMovesLearn (progress_position_moves_learn.py:37-62),
+ * step 1: the ordered update stream of n games.  Game g's recorded positions
+ * (an oth_replay layout: row g*OTH_POS_STRIDE + p, p = 0..plies[g]) are visited
+ * as learn_books orders a book (sorted by turn, reversed: terminal first,
+ * replearn.py:36-38) and __update_state_for_a_book walks it (sides 'O' then
+ * 'X'): update j = base[g] + 2*(plies[g] - p) + (0 for 'O', 1 for 'X') gets
+ *   keys[j]   = OTH_TD_KEY(counts(position p, side))      (hash_from_book)
+ *   values[j] = (double)value_side * lam_pow[plies[g] - p]   (value * l ** turn_left)
+ * with value_O = n_black - n_white of the terminal position and value_X its
+ * negation (41-42).  base (n, exclusive prefix sum of 2*(plies+1)) and lam_pow
+ * (OTH_POS_STRIDE doubles, lam_pow[k] = l ** k as the host computes it) are
+ * device arrays. */
+#define OTH_TD_KEY_BITS 54
+/* packed counts() key: discs << 47 | moves << 40 | regions a..h, 5 bits each
+ * from bit 35 down to bit 0.  Integer order == tuple order. */
+int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
+                   int64_t* keys, double* values, int64_t n, void* stream);
+
+/* TD state map, step 2: segment s (updates seg_off[s] .. seg_off[s+1]-1 of one
+ * key, in stream order) starts from init[s] and applies, in order,
+ *   v = (v == 0) ? x : v * one_minus_a + x * a          (58-61; no fused multiply-add)
+ * out[s] = final v.  All arrays are device memory. */
+int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,
+               double* out, int64_t n_seg, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

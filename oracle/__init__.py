@@ -195,3 +195,27 @@ def game_key(seed, g):
 def rng_draw(key, i):
     """The i-th (1-based) draw of game key `key`'s LCG stream."""
     return lib().oracle_rng_draws(key, i)
+
+
+def td_state_map(pos_boards, plies, store=None, a=0.03, lam=0.90):
+    """progress_position_moves_learn.py:37-62 restated over the oracle's counts():
+    books = games in order, each walked terminal -> opening, sides 'O' then 'X'.
+    pos_boards (n, 129, 2) uint64 replay rows, plies (n,).  Returns {counts tuple:
+    value} (pure-Python EMA loop: small cases only)."""
+    store = {} if store is None else store
+    pos_boards = np.asarray(pos_boards, np.uint64)
+    n = len(plies)
+    for g in range(n):
+        np_ = min(int(plies[g]), MOVES_STRIDE)
+        rows = np.ascontiguousarray(pos_boards[g, :np_ + 1])
+        fb = features(rows, np.full(np_ + 1, 1, np.uint8))
+        fw = features(rows, np.full(np_ + 1, 2, np.uint8))
+        term = rows[np_]
+        vb = bin(int(term[0])).count("1") - bin(int(term[1])).count("1")
+        for p in range(np_, -1, -1):
+            for f, value in ((fb[p], vb), (fw[p], -vb)):
+                key = tuple(int(x) for x in f)
+                cur = float(store.get(key, 0))
+                new = float(value) * (lam ** (np_ - p))
+                store[key] = new if cur == 0 else cur * (1 - a) + new * a
+    return store

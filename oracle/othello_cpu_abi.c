@@ -119,6 +119,58 @@ int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int6
     return oracle_features(boards, side, out, n);
 }
 
+/* TD update stream over the oracle's counts() (see include/othello.h) */
+static int64_t td_key(const uint8_t f[10]) {
+    static const int shift[10] = {47, 40, 35, 30, 25, 20, 15, 10, 5, 0};
+    int64_t k = 0;
+    for (int i = 0; i < 10; i++) k |= (int64_t)f[i] << shift[i];
+    return k;
+}
+
+int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
+                   int64_t* keys, double* values, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
+    for (int64_t g = 0; g < n; g++) {
+        const uint64_t* row = pos_boards + g * OTH_POS_STRIDE * 2;
+        const int np = plies[g] < OTH_MOVES_STRIDE ? plies[g] : OTH_MOVES_STRIDE;
+        int8_t d;
+        oracle_result(row + 2 * np, NULL, NULL, &d, NULL, 1);
+        for (int p = 0; p <= np; p++) {
+            uint8_t f[2][10];
+            const uint8_t sides[2] = {OTH_BLACK, OTH_WHITE};
+            const uint64_t b2[4] = {row[2 * p], row[2 * p + 1], row[2 * p], row[2 * p + 1]};
+            oracle_features(b2, sides, &f[0][0], 2);
+            const int64_t j = base[g] + 2 * (int64_t)(np - p);
+            keys[j] = td_key(f[0]);
+            values[j] = (double)d * lam_pow[np - p];
+            keys[j + 1] = td_key(f[1]);
+            values[j + 1] = (double)(-d) * lam_pow[np - p];
+        }
+    }
+    return OTH_OK;
+}
+
+int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,
+               double* out, int64_t n_seg, void* stream) {
+    (void)stream;
+    if (n_seg < 0 || (n_seg > 0 && (!values || !seg_off || !out))) return OTH_EINVAL;
+    for (int64_t s = 0; s < n_seg; s++) {
+        double v = init ? init[s] : 0.0;
+        for (int64_t i = seg_off[s]; i < seg_off[s + 1]; i++) {
+            const double x = values[i];
+            if (v == 0.0) {
+                v = x;
+            } else {
+                const double t1 = v * one_minus_a, t2 = x * a;
+                v = t1 + t2;
+            }
+        }
+        out[s] = v;
+    }
+    return OTH_OK;
+}
+
 int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
              void* stream) {
     (void)stream;

@@ -20,6 +20,7 @@ BOOK_LINE = 67
 N_FEATURES = 10
 POLICY_RANDOM, POLICY_GREEDY, POLICY_EVAL = 0, 1, 2
 EVAL_PHASES, EVAL_FEATURES, EVAL_WEIGHTS = 4, 9, 36
+TD_KEY_BITS = 54
 
 # name -> (restype, argtypes); must match include/othello.h exactly
 _P, _I64, _U64, _I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
@@ -36,6 +37,8 @@ SIGNATURES = {
     "oth_features": (_I, [_P, _P, _P, _I64, _P]),
     "oth_rollout_eval": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_eval": (_I, [_P, _P, _P, _P, _I64, _P]),
+    "oth_td_updates": (_I, [_P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),
 }
 
 

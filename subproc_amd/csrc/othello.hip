@@ -570,6 +570,61 @@ __global__ __launch_bounds__(kBlock) void eval_kernel(const u64* __restrict__ bo
     out[i] = eval_linear(w, mine, mob);
 }
 
+// ---------------------------------------------------------------------------
+// TD state map (progress_position_moves_learn.py:37-62), include/othello.h
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t td_key(ulonglong2 b, u32 sd) {
+    u64 mine, mob;
+    side_view(b, sd, mine, mob);
+    u64 k = ((u64)__popcll(b.x | b.y) << 47) | ((u64)__popcll(mob) << 40);
+#pragma unroll
+    for (int r = 0; r < 8; r++) k |= (u64)__popcll(mine & kRegionMasks[r]) << (35 - 5 * r);
+    return (int64_t)k;
+}
+
+// one thread per recorded position (g, p)
+__global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restrict__ pos,
+                                                            const uint8_t* __restrict__ plies,
+                                                            const int64_t* __restrict__ base,
+                                                            const double* __restrict__ lam_pow,
+                                                            int64_t* __restrict__ keys, double* __restrict__ vals,
+                                                            int64_t n) {
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= n * OTH_POS_STRIDE) return;
+    const int64_t g = idx / OTH_POS_STRIDE;
+    const u32 p = (u32)(idx - g * OTH_POS_STRIDE);
+    const u32 np = min<u32>(plies[g], OTH_MOVES_STRIDE);
+    if (p > np) return;
+    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + g * OTH_POS_STRIDE;
+    const ulonglong2 term = row[np];
+    const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
+    const ulonglong2 b = row[p];
+    const double lam = lam_pow[np - p];
+    const int64_t j = base[g] + 2 * (int64_t)(np - p);
+    keys[j] = td_key(b, OTH_BLACK);
+    vals[j] = (double)vb * lam;
+    keys[j + 1] = td_key(b, OTH_WHITE);
+    vals[j + 1] = (double)(-vb) * lam;
+}
+
+// one thread per key segment, strictly sequential in stream order (the EMA is
+// order-dependent and bit-exact parity needs Python's rounding: no contraction)
+__global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
+                                                        const int64_t* __restrict__ seg_off,
+                                                        const double* __restrict__ init, double a, double oma,
+                                                        double* __restrict__ out, int64_t n_seg) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n_seg) return;
+    double v = init ? init[s] : 0.0;
+    const int64_t e = seg_off[s + 1];
+    for (int64_t i = seg_off[s]; i < e; i++) {
+        const double x = vals[i];
+        v = (v == 0.0) ? x : v * oma + x * a;
+    }
+    out[s] = v;
+}
+
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
 
 // launch geometry of the rollout kernel, resolved once per process (device 0 of
@@ -762,6 +817,24 @@ int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights,
     EvalWeights ew;
     for (int k = 0; k < OTH_EVAL_WEIGHTS; k++) ew.w[k] = weights[k];
     eval_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards, side, ew, out, n);
+    return launched();
+}
+
+int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
+                   int64_t* keys, double* values, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, plies, base,
+                                                                                          lam_pow, keys, values, n);
+    return launched();
+}
+
+int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,
+               double* out, int64_t n_seg, void* stream) {
+    if (n_seg < 0 || (n_seg > 0 && (!values || !seg_off || !out))) return OTH_EINVAL;
+    if (n_seg == 0) return OTH_OK;
+    td_ema_kernel<<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a, out,
+                                                                         n_seg);
     return launched();
 }
 

@@ -1,0 +1,139 @@
+"""TD state map of the progress/position/moves learner on the GPU.
+
+ProgressPositionMovesLearn keeps, per ``counts()`` hash, an exponentially
+averaged TD target in the parameter store, one Redis round trip per position and
+side (progress_position_moves_learn.py:37-62):
+
+    for book in books:                    # learn_books order; each book terminal-first
+        last_turn, v_O = terminal nturn, n_black - n_white (v_X = -v_O)
+        for record in book:               # terminal -> opening
+            for side, value in (('O', v_O), ('X', v_X)):
+                new = value * l ** (last_turn - turn)
+                v[key] = new if v[key] == 0 else v[key] * (1 - a) + new * a
+
+Here the whole batch runs on the device:
+  1. ``oth_td_updates`` (HIP) emits the ordered update stream: packed counts()
+     key + value per (position, side), from an ``oth_replay`` position table;
+  2. a stable sort by key (torch) groups each key's updates in stream order;
+  3. ``oth_td_ema`` (HIP) replays each key's updates sequentially in float64
+     with separate multiply and add, so every value is bit-identical to the
+     Python learner's;
+  4. the result is merged into the device-resident, key-sorted table.
+Batches applied one after another equal one batch of all their books.
+Redis/sampling/regression stay out of scope; values are kept as float64 (the
+Python learner's float, before any store round trip).
+"""
+import torch
+
+from . import _lib
+from ._lib import POS_STRIDE, check
+
+A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
+LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
+_SHIFTS = (47, 40, 35, 30, 25, 20, 15, 10, 5, 0)
+_WIDTH = (7, 7, 5, 5, 5, 5, 5, 5, 5, 5)
+
+
+def lam_pow_table(lam=LAMBDA):
+    """l ** k for k = 0..128 as CPython computes it (the learner's own pow)."""
+    return [lam ** k for k in range(POS_STRIDE)]
+
+
+def counts_to_key(c):
+    """Pack a counts() 10-tuple (include/othello.h OTH_TD_KEY_BITS layout)."""
+    k = 0
+    for v, s, w in zip(c, _SHIFTS, _WIDTH):
+        if not 0 <= int(v) < (1 << w):
+            raise ValueError(f"counts value {v} out of range")
+        k |= int(v) << s
+    return k
+
+
+def key_to_counts(k):
+    k = int(k)
+    return tuple((k >> s) & ((1 << w) - 1) for s, w in zip(_SHIFTS, _WIDTH))
+
+
+def hash_string(k):
+    """ProgressPositionMovesParameter.hash_from_book format (parameter_progress_position_moves_learn.py:47-49)."""
+    return ":".join(str(v) for v in key_to_counts(k))
+
+
+class StateMap:
+    """Device-resident 'param:state:*' table: sorted int64 keys + float64 values."""
+
+    def __init__(self, device="cuda", a=A, lam=LAMBDA):
+        d = torch.device(device)
+        if d.type == "cuda" and d.index is None:
+            d = torch.device("cuda", torch.cuda.current_device())
+        self.device = d
+        self.a = a
+        self.lam = lam
+        self.keys = torch.empty(0, dtype=torch.int64, device=self.device)
+        self.values = torch.empty(0, dtype=torch.float64, device=self.device)
+        self._lam_pow = torch.tensor(lam_pow_table(lam), dtype=torch.float64, device=self.device)
+
+    def __len__(self):
+        return int(self.keys.numel())
+
+    def update(self, pos_boards, plies):
+        """Apply the books of n games: pos_boards (n, 129, 2) int64 as ops.replay
+        returns it, plies (n,) uint8.  Returns the number of updates applied."""
+        n = plies.shape[0]
+        if pos_boards.shape != (n, POS_STRIDE, 2) or pos_boards.dtype != torch.int64:
+            raise ValueError("pos_boards must be an (n, 129, 2) int64 replay table")
+        if plies.dtype != torch.uint8 or pos_boards.device != self.device or plies.device != self.device:
+            raise ValueError("plies must be uint8; both on the map's device")
+        if n == 0:
+            return 0
+        cnt = 2 * (plies.long().clamp(max=POS_STRIDE - 1) + 1)
+        ends = torch.cumsum(cnt, 0)
+        base = (ends - cnt).contiguous()
+        total = int(ends[-1])
+        keys = torch.empty(total, dtype=torch.int64, device=self.device)
+        vals = torch.empty(total, dtype=torch.float64, device=self.device)
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
+            check(lib.oth_td_updates(pos_boards.contiguous().data_ptr(), plies.contiguous().data_ptr(),
+                                     base.data_ptr(), self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n,
+                                     stream), "oth_td_updates")
+            sk, perm = torch.sort(keys, stable=True)
+            sv = vals[perm].contiguous()
+            ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
+            seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
+            torch.cumsum(counts, 0, out=seg_off[1:])
+            init = torch.zeros(ukeys.numel(), dtype=torch.float64, device=self.device)
+            found = idx = None
+            if len(self):
+                idx = torch.searchsorted(self.keys, ukeys).clamp(max=len(self) - 1)
+                found = self.keys[idx] == ukeys
+                init[found] = self.values[idx[found]]
+            out = torch.empty_like(init)
+            check(lib.oth_td_ema(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
+                                 out.data_ptr(), ukeys.numel(), stream), "oth_td_ema")
+            if found is None:
+                self.keys, self.values = ukeys, out
+            else:
+                self.values[idx[found]] = out[found]
+                allk = torch.cat([self.keys, ukeys[~found]])
+                allv = torch.cat([self.values, out[~found]])
+                self.keys, p = torch.sort(allk)
+                self.values = allv[p]
+        return total
+
+    def update_from_books(self, books):
+        """Apply a subproc_amd.books.GameBooks batch."""
+        return self.update(books.pos.boards, books.plies)
+
+    def get(self, counts):
+        """Value for a counts() tuple, 0.0 if absent (a fresh key reads as 0, 53-56)."""
+        k = torch.tensor([counts_to_key(counts)], dtype=torch.int64, device=self.device)
+        if not len(self):
+            return 0.0
+        i = int(torch.searchsorted(self.keys, k).clamp(max=len(self) - 1))
+        return float(self.values[i]) if int(self.keys[i]) == int(k) else 0.0
+
+    def items(self):
+        """{hash_from_book string: value} on the host."""
+        return {hash_string(k): v for k, v in zip(self.keys.cpu().tolist(), self.values.cpu().tolist())}

@@ -479,6 +479,43 @@ def main():
                       "lines": lines, "records": records, "counts": feats})
     json.dump(books, open(os.path.join(OUT, "books.json"), "w"))
 
+    # ---------------------------------------------------------------- TD state map (§8f row 2)
+    # ProgressPositionMovesLearn.__update_state_for_a_book / __update_state_map
+    # (progress_position_moves_learn.py:37-62) over the 256 rollout_random games as
+    # learn_books hands them over (replearn.py:34-39: records sorted by turn,
+    # reversed).  The key is the reference's own hash_from_book and the terminal
+    # value uses its board_from_a_book; the module itself imports pyres/slack
+    # (absent), so only the five EMA lines are restated here.
+    param = ns["ProgressPositionMovesParameter"]()
+    bfab = ns["board_from_a_book"]
+    a_, l_ = 0.03, 0.90  # ProgressPositionMovesLearn.__init__ (22-24)
+    store = {}
+    for g in range(len(z["plies"])):
+        b = from_bits(ib, iw, Black)
+        recs = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                 "end": b.is_game_over()}]
+        for code in z["moves"][g]:
+            if code == 255:
+                break
+            assert b.put_s(code_to_str(b, int(code))) >= 0
+            recs.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                         "end": b.is_game_over()})
+        book = list(reversed(sorted(recs, key=lambda x: int(x["turn"]))))
+        last_turn = int(book[0]["turn"])
+        last_board = bfab(book[0])
+        vb = last_board.n_black() - last_board.n_white()
+        vw = last_board.n_white() - last_board.n_black()
+        for rec in book:
+            for side, value in (("O", vb), ("X", vw)):
+                key = param.hash_from_book(rec, side)
+                cur = float(store.get(key, 0))
+                new = float(value) * (l_ ** (last_turn - int(rec["turn"])))
+                store[key] = new if cur == 0 else cur * (1 - a_) + new * a_
+    ks = sorted(store)
+    np.savez_compressed(os.path.join(OUT, "td_state.npz"), source=np.array("rollout_random"),
+                        games=np.array(len(z["plies"])), hash=np.array(ks), value=np.array([store[k] for k in ks]),
+                        draws=np.array(int((z["diff"] == 0).sum())))
+
     # ---------------------------------------------------------------- RNG known answers
     S = seed_state(SEED)
     r0 = GameRng(game_key(S, 0))

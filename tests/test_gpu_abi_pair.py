@@ -24,7 +24,7 @@ class Buf:
     def __init__(self, a):
         self.h = np.ascontiguousarray(a)
         dt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint8: torch.uint8, np.int8: torch.int8,
-              np.int32: torch.int32}[self.h.dtype.type]
+              np.int32: torch.int32, np.float64: torch.float64}[self.h.dtype.type]
         src = self.h.view(np.int64) if self.h.dtype == np.uint64 else self.h
         self.d = torch.from_numpy(src.copy()).to(dt).to(DEV)
 
@@ -113,3 +113,29 @@ def test_books_features_eval_pair():
     w = (ctypes.c_int8 * 36)(*np.random.default_rng(3).integers(-128, 128, 36).tolist())
     both("oth_eval", flat_b, side, w, ev, k)
     same(feats, ev)
+
+
+def test_td_pair():
+    n = 256
+    plies = Buf(np.zeros(n, np.uint8))
+    moves = Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8))
+    both("oth_rollout", None, None, 21, 0, 1, 4, None, None, plies, moves, None, n)
+    same(plies, moves)
+    pos = Buf(np.zeros((n, _lib.POS_STRIDE, 2), np.uint64))
+    both("oth_replay", None, None, moves, plies, pos, None, None, n)
+    same(pos)
+    cnt = 2 * (plies.h.astype(np.int64) + 1)
+    base = Buf(np.cumsum(cnt) - cnt)
+    lam = Buf(np.array([0.9 ** k for k in range(_lib.POS_STRIDE)], np.float64))
+    total = int(cnt.sum())
+    keys, vals = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+    both("oth_td_updates", pos, plies, base, lam, keys, vals, n)
+    same(keys, vals)
+    order = np.argsort(keys.h, kind="stable")
+    uk, starts = np.unique(keys.h[order], return_index=True)
+    sv = Buf(vals.h[order])
+    seg = Buf(np.append(starts, total).astype(np.int64))
+    init = Buf(np.random.default_rng(4).choice([0.0, 0.5, -1.25], len(uk)))
+    out = Buf(np.zeros(len(uk), np.float64))
+    both("oth_td_ema", sv, seg, init, 0.03, 1 - 0.03, out, len(uk))
+    same(out)

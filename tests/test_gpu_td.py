@@ -1,0 +1,48 @@
+"""TD state map on the GPU: oth_td_updates + stable sort +
+oth_td_ema must reproduce the learner's float64 values bit-exactly."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from golden_io import load_npz
+from subproc_amd import ops, td
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_state_map_matches_reference_fixture_and_batches_compose():
+    z = load_npz("rollout_random.npz")
+    f = load_npz("td_state.npz")
+    want = {h: float(v) for h, v in zip(f["hash"].tolist(), f["value"])}
+    moves = torch.from_numpy(z["moves"]).to(DEV)
+    plies = torch.from_numpy(z["plies"]).to(DEV)
+    pos = ops.replay(moves, plies)
+    sm = td.StateMap(DEV)
+    assert sm.update(pos.boards, plies) == int(2 * (z["plies"].astype(np.int64) + 1).sum())
+    assert sm.items() == want
+    # the same books in three batches
+    sm2 = td.StateMap(DEV)
+    for lo, hi in ((0, 1), (1, 100), (100, 256)):
+        sm2.update(pos.boards[lo:hi].contiguous(), plies[lo:hi].contiguous())
+    assert sm2.items() == want
+    k = next(iter(want))
+    assert sm.get(tuple(int(x) for x in k.split(":"))) == want[k]
+    assert sm.get((64, 0, 0, 0, 0, 0, 0, 0, 0, 0)) == 0.0
+
+
+def test_state_map_at_scale_vs_oracle():
+    """4096 random + 1024 greedy games (greedy ones start mid-game-like sequences
+    of repeated keys) against the Python restatement over the C oracle."""
+    r1 = ops.rollout(4096, 17, 0, "random", record_moves=True, device=DEV)
+    r2 = ops.rollout(1024, 18, 0, "greedy", 10, record_moves=True, device=DEV)
+    sm = td.StateMap(DEV)
+    store = {}
+    for r in (r1, r2):
+        pos = ops.replay(r.moves, r.plies)
+        sm.update(pos.boards, r.plies)
+        store = oracle.td_state_map(ops.to_numpy_u64(pos.boards), r.plies.cpu().numpy(), store)
+    got = {td.key_to_counts(k): v for k, v in zip(sm.keys.cpu().tolist(), sm.values.cpu().tolist())}
+    assert got == store
+    assert torch.all(sm.keys[1:] > sm.keys[:-1])  # table stays sorted and unique

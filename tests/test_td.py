@@ -1,0 +1,72 @@
+"""TD state map (progress_position_moves_learn.py:37-62):
+host side — key packing, the oracle restatement and the CPU build of the
+header's oth_td_* against the fixture made with the reference's hash_from_book."""
+import ctypes
+
+import numpy as np
+
+import oracle
+from golden_io import load_npz
+from subproc_amd import _lib, td
+
+P = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+
+
+def fixture():
+    z = load_npz("td_state.npz")
+    return {tuple(int(x) for x in h.split(":")): float(v) for h, v in zip(z["hash"], z["value"])}
+
+
+def fixture_games():
+    z = load_npz("rollout_random.npz")
+    pos = oracle.replay(z["moves"], z["plies"])
+    return pos["boards"], z["plies"]
+
+
+def test_key_packing():
+    for c in [(4, 4, 0, 0, 0, 0, 0, 0, 0, 2), (64, 0, 4, 8, 4, 8, 8, 16, 4, 12), (64, 99, 0, 0, 0, 0, 0, 0, 0, 0)]:
+        k = td.counts_to_key(c)
+        assert td.key_to_counts(k) == c and k < (1 << _lib.TD_KEY_BITS)
+        assert td.hash_string(k) == ":".join(map(str, c))
+    # integer order == tuple order
+    cs = [(5, 3, 1, 0, 0, 0, 0, 0, 0, 0), (5, 3, 0, 9, 9, 9, 9, 9, 9, 9), (4, 40, 4, 8, 4, 8, 8, 16, 4, 12)]
+    assert sorted(cs) == sorted(cs, key=td.counts_to_key)
+
+
+def test_lam_pow_is_cpython_pow():
+    t = td.lam_pow_table()
+    assert t[0] == 1.0 and t[1] == 0.9 and t[61] == 0.9 ** 61 and len(t) == _lib.POS_STRIDE
+
+
+def test_oracle_state_map_matches_reference_fixture():
+    boards, plies = fixture_games()
+    got = oracle.td_state_map(boards, plies)
+    assert got == fixture()  # float equality: bit-exact
+
+
+def test_cpu_abi_td_matches_fixture_and_batches_compose():
+    boards, plies = fixture_games()
+    lib = oracle.cpu_abi()
+    lam = np.array(td.lam_pow_table(), np.float64)
+
+    def run(b, pl, state):
+        n = len(pl)
+        cnt = 2 * (pl.astype(np.int64) + 1)
+        base = np.ascontiguousarray(np.cumsum(cnt) - cnt)
+        keys, vals = np.empty(int(cnt.sum()), np.int64), np.empty(int(cnt.sum()), np.float64)
+        assert lib.oth_td_updates(P(np.ascontiguousarray(b)), P(np.ascontiguousarray(pl)), P(base), P(lam), P(keys),
+                                  P(vals), n, None) == 0
+        order = np.argsort(keys, kind="stable")
+        sk, sv = keys[order], np.ascontiguousarray(vals[order])
+        uk, starts, counts = np.unique(sk, return_index=True, return_counts=True)
+        seg = np.ascontiguousarray(np.append(starts, len(sk)).astype(np.int64))
+        init = np.ascontiguousarray([state.get(int(k), 0.0) for k in uk], np.float64)
+        out = np.empty(len(uk), np.float64)
+        assert lib.oth_td_ema(P(sv), P(seg), P(init), 0.03, 1 - 0.03, P(out), len(uk), None) == 0
+        state.update({int(k): float(v) for k, v in zip(uk, out)})
+        return state
+
+    want = {td.counts_to_key(k): v for k, v in fixture().items()}
+    assert run(boards, plies, {}) == want
+    s = run(boards[:100], plies[:100], {})
+    assert run(boards[100:], plies[100:], s) == want

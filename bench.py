@@ -17,6 +17,7 @@ Also reported on rank 0 (secondary, same JSON line):
   * greedy     : config 5, 1,048,576 1-ply greedy-mobility games;
   * eval       : 1,048,576 games of the 1-ply linear-eval policy with the
     learner's default weights (SURVEY.md §8f row 2);
+  * td_state_map: the learner's TD state-map update for 262,144 GPU games;
   * cpu_baseline: the C oracle (mailbox restatement of board.py) on a bounded
     sample of the same workload on the host cores.
 
@@ -215,6 +216,7 @@ def main():
         if args.workload != "greedy":
             sec["greedy_1M"] = _bench_greedy(ops, torch, dev, stream, args)
         sec["eval_1M"] = _bench_greedy(ops, torch, dev, stream, args, policy="eval")
+        sec["td_state_map"] = _bench_td(ops, torch, dev, args)
         out["secondary"] = sec
         out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
     if rank == 0:
@@ -280,6 +282,26 @@ def _bench_greedy(ops, torch, dev, stream, args, policy="greedy"):
     what = "greedy-mobility" if policy == "greedy" else "linear-eval (learner default weights)"
     return {"metric": f"env-steps/sec ({what} self-play)", "value": int(hist[132]) / dt,
             "unit": "env-steps/s", "games": n, "ms": dt * 1e3}
+
+
+def _bench_td(ops, torch, dev, args, games=1 << 18):
+    """§8f row 2: the learner's TD state-map update for a batch of GPU self-play
+    books (replay + ordered update stream + stable sort + per-key EMA + merge
+    into a table that already holds one batch)."""
+    from subproc_amd.td import StateMap
+
+    r = ops.rollout(games, args.seed, 1 << 41, "random", record_moves=True, device=dev)
+    r2 = ops.rollout(games, args.seed, (1 << 41) + games, "random", record_moves=True, device=dev)
+    sm = StateMap(dev)
+    sm.update(ops.replay(r.moves, r.plies).boards, r.plies)  # warm-up batch (and a non-empty table)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pos = ops.replay(r2.moves, r2.plies)
+    n_upd = sm.update(pos.boards, r2.plies)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "TD state-map updates/sec (position x side, learner order)", "value": n_upd / dt,
+            "unit": "updates/s", "games": games, "updates": n_upd, "keys": len(sm), "ms": dt * 1e3}
 
 
 def _cpu_baseline(args, workload):

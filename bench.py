@@ -287,14 +287,16 @@ def _bench_greedy(ops, torch, dev, stream, args, policy="greedy"):
 def _bench_td(ops, torch, dev, args, games=1 << 18):
     """§8f row 2: the learner's TD state-map update for a batch of GPU self-play
     books (replay + ordered update stream + stable sort + per-key EMA + merge
-    into a table that already holds one batch)."""
+    into a table that already holds two batches)."""
     from subproc_amd.td import StateMap
 
-    r = ops.rollout(games, args.seed, 1 << 41, "random", record_moves=True, device=dev)
-    r2 = ops.rollout(games, args.seed, (1 << 41) + games, "random", record_moves=True, device=dev)
+    rs = [ops.rollout(games, args.seed, (1 << 41) + k * games, "random", record_moves=True, device=dev)
+          for k in range(3)]
     sm = StateMap(dev)
-    sm.update(ops.replay(r.moves, r.plies).boards, r.plies)  # warm-up batch (and a non-empty table)
+    for r in rs[:2]:  # warm-up: the empty-table path, then the merge path (first-use kernel loading)
+        sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
     torch.cuda.synchronize()
+    r2 = rs[2]
     t0 = time.perf_counter()
     pos = ops.replay(r2.moves, r2.plies)
     n_upd = sm.update(pos.boards, r2.plies)

@@ -104,23 +104,47 @@ class StateMap:
             seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
             torch.cumsum(counts, 0, out=seg_off[1:])
             init = torch.zeros(ukeys.numel(), dtype=torch.float64, device=self.device)
-            found = idx = None
+            pos_in_old = None
             if len(self):
-                idx = torch.searchsorted(self.keys, ukeys).clamp(max=len(self) - 1)
-                found = self.keys[idx] == ukeys
-                init[found] = self.values[idx[found]]
+                pos_in_old = torch.searchsorted(self.keys, ukeys)  # old keys < each update key
+                cl = pos_in_old.clamp(max=len(self) - 1)
+                init = torch.where(self.keys[cl] == ukeys, self.values[cl], init)
             out = torch.empty_like(init)
             check(lib.oth_td_ema(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
                                  out.data_ptr(), ukeys.numel(), stream), "oth_td_ema")
-            if found is None:
+            if pos_in_old is None:
                 self.keys, self.values = ukeys, out
             else:
-                self.values[idx[found]] = out[found]
-                allk = torch.cat([self.keys, ukeys[~found]])
-                allv = torch.cat([self.values, out[~found]])
-                self.keys, p = torch.sort(allk)
-                self.values = allv[p]
+                self._merge(pos_in_old, ukeys, out)
         return total
+
+    def _merge(self, pos_in_old, ukeys, out):
+        """Merge the updated keys (sorted, unique) into the table (sorted) by
+        rank, with gathers and scatters only (no compaction, no re-sort):
+          old key i    -> slot i + (new keys below it)
+          update key j -> slot (new keys before j) + (old keys below it)
+        A key in both lists gets the same slot and the same (key, value) from
+        both sides, so the duplicate write is benign."""
+        n_old, n_upd = len(self), ukeys.numel()
+        rank_in_upd = torch.searchsorted(ukeys, self.keys)  # update keys < each old key
+        cl = rank_in_upd.clamp(max=n_upd - 1)
+        hit = ukeys[cl] == self.keys
+        new_before = torch.zeros(n_upd + 1, dtype=torch.int64, device=self.device)
+        torch.cumsum((self.keys[pos_in_old.clamp(max=n_old - 1)] != ukeys).long(), 0, out=new_before[1:])
+        n_new = int(new_before[-1])
+        old_vals = torch.where(hit, out[cl], self.values)
+        if n_new == 0:
+            self.values = old_vals
+            return
+        pos_old = torch.arange(n_old, device=self.device) + new_before[rank_in_upd]
+        pos_upd = new_before[:-1] + pos_in_old
+        keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
+        vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
+        keys[pos_old] = self.keys
+        vals[pos_old] = old_vals
+        keys[pos_upd] = ukeys
+        vals[pos_upd] = out
+        self.keys, self.values = keys, vals
 
     def update_from_books(self, books):
         """Apply a subproc_amd.books.GameBooks batch."""

@@ -46,3 +46,35 @@ def test_state_map_at_scale_vs_oracle():
     got = {td.key_to_counts(k): v for k, v in zip(sm.keys.cpu().tolist(), sm.values.cpu().tolist())}
     assert got == store
     assert torch.all(sm.keys[1:] > sm.keys[:-1])  # table stays sorted and unique
+
+
+def test_td_ema_zero_states_in_long_segments():
+    """oth_td_ema speculates that no state in a 16-update chunk is exactly 0 and
+    redoes the chunk otherwise: plant exact zero states (a = 0.5, x = -v) at
+    chunk starts, middles and ends of long segments and compare with the
+    sequential rule in Python floats."""
+    from subproc_amd import _lib
+    a, oma = 0.5, 0.5
+    rng = np.random.default_rng(11)
+    lengths = [1, 5, 47, 48, 49, 63, 64, 100, 1000, 4099]
+    vals, seg, want = [], [0], []
+    for L in lengths:
+        v = 0.0 if L % 2 else 0.25
+        init_v = v
+        zero_at = set(rng.choice(L, size=min(L, 9), replace=False).tolist()) | {15, 16, 47, 48}
+        for k in range(L):
+            x = float(rng.normal())
+            if k in zero_at and v != 0.0:
+                x = -v  # v * 0.5 + (-v) * 0.5 == 0 exactly
+            vals.append(x)
+            v = x if v == 0.0 else v * oma + x * a
+        seg.append(len(vals))
+        want.append((init_v, v))
+    init = torch.tensor([w[0] for w in want], dtype=torch.float64, device=DEV)
+    dv = torch.tensor(vals, dtype=torch.float64, device=DEV)
+    ds = torch.tensor(seg, dtype=torch.int64, device=DEV)
+    out = torch.empty(len(lengths), dtype=torch.float64, device=DEV)
+    lib = _lib.load()
+    _lib.check(lib.oth_td_ema(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(), len(lengths),
+                              torch.cuda.current_stream().cuda_stream), "oth_td_ema")
+    assert out.cpu().tolist() == [w[1] for w in want]

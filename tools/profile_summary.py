@@ -21,9 +21,10 @@ N_SIMD = 1024
 
 
 def short(name):
-    for k in ("rollout_kernel<0, false>", "rollout_kernel<1, false>", "rollout_kernel<0, true>",
-              "rollout_kernel<1, true>", "step_kernel", "legal_kernel", "result_kernel", "reset_kernel",
-              "sample_midgame_kernel"):
+    for k in ("rollout_kernel<0, false>", "rollout_kernel<1, false>", "rollout_kernel<2, false>",
+              "rollout_kernel<0, true>", "rollout_kernel<1, true>", "rollout_kernel<2, true>", "step_kernel",
+              "legal_kernel", "result_kernel", "reset_kernel", "sample_midgame_kernel", "replay_kernel",
+              "book_text_kernel", "features_kernel", "eval_kernel", "td_updates_kernel", "td_ema_kernel"):
         if k in name:
             return k
     return None

@@ -7,8 +7,9 @@
 //   * 64-bit shifts stay single v_lshl/v_lshrrev_b64 instructions;
 //   * every fill step / flip accumulation is one v_bfi_b32 per 32-bit half (see bfi);
 //   * Kogge-Stone propagators are computed once per position and shared between
-//     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S) and between legal-move
-//     generation and flip computation.
+//     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S);
+//   * the chosen move's flips come from per-square ray tables in LDS and the
+//     run sets of the analysis (flips_rays), not from more fills.
 //
 // Square sq = x + 8*y (board.py:74-81); rays of board.py:9-17 as shifts:
 //   +1 R (x+1), +8 D (y+1), +9 RD, +7 LD   and their opposites -1 L, -8 U, -9 LU, -7 RU.
@@ -53,24 +54,6 @@ __device__ __forceinline__ PairProp pair_prop(u64 pro) {
     return q;
 }
 
-// An empty asm that hides a value's provenance (emits no instruction).  Used on
-// propagators shared between legal-move generation and flips: otherwise hipcc
-// CSEs their complements (one v_not each, kept live) and rewrites every bfi of
-// the flip fills into and + or.
-__device__ __forceinline__ u64 opaque(u64 x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ PairProp opaque(const PairProp& q) {
-    PairProp r;
-    r.pro = opaque(q.pro);
-    r.p2L = opaque(q.p2L);
-    r.p4L = opaque(q.p4L);
-    r.p2R = opaque(q.p2R);
-    r.p4R = opaque(q.p4R);
-    return r;
-}
-
 // occluded fill of `gen` along +S (L) or -S through the pair's propagators:
 // covers distances 0..7
 template <int S, bool L>
@@ -98,8 +81,7 @@ __device__ __forceinline__ u64 rev64(u64 x) {
 // opponent discs only (board.py:124-139's "hostile" runs, seen from P).
 // Direction index i: 0:+1 1:-1 2:+8 3:-8 4:+9 5:-9 6:+7 7:-7
 struct Position {
-    PairProp v, d9, d7;  // the horizontal pair needs no propagators (carry tricks)
-    u64 Oi, rOi;          // inner opponent discs, and bit-reversed
+    u64 Oi, rOi;  // inner opponent discs, and bit-reversed
     u64 A[8];
     u64 reach;  // squares one step beyond an attached run (any content)
     u64 legal;  // Board.puttables as a mask (board.py:46-52) = reach & empty
@@ -109,9 +91,8 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     const u64 Oi = O & INNER_FILES;
     s.Oi = Oi;
     s.rOi = rev64(Oi);
-    s.v = pair_prop<8>(O);
-    s.d9 = pair_prop<9>(Oi);
-    s.d7 = pair_prop<7>(Oi);
+    // the horizontal pair needs no propagators (carry tricks below)
+    const PairProp v = pair_prop<8>(O), d9 = pair_prop<9>(Oi), d7 = pair_prop<7>(Oi);
     // east (+1): bits along the ray are contiguous, so one add propagates a
     // carry from each P disc through its adjacent run of inner opponent discs
     // and clears exactly those run bits: A = Oi & ~(Oi + (P << 1)).
@@ -119,12 +100,12 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     // west (-1): the same on the bit-reversed board
     s.A[1] = rev64(east_run(rev64(P), s.rOi));
     // the Kogge-Stone fills from P stay inside P | O, so "minus P" is "and O"
-    s.A[2] = ks<8, true>(P, s.v) & O;
-    s.A[3] = ks<8, false>(P, s.v) & O;
-    s.A[4] = ks<9, true>(P, s.d9) & O;
-    s.A[5] = ks<9, false>(P, s.d9) & O;
-    s.A[6] = ks<7, true>(P, s.d7) & O;
-    s.A[7] = ks<7, false>(P, s.d7) & O;
+    s.A[2] = ks<8, true>(P, v) & O;
+    s.A[3] = ks<8, false>(P, v) & O;
+    s.A[4] = ks<9, true>(P, d9) & O;
+    s.A[5] = ks<9, false>(P, d9) & O;
+    s.A[6] = ks<7, true>(P, d7) & O;
+    s.A[7] = ks<7, false>(P, d7) & O;
     // a legal square is one step beyond an attached run, and empty
     u64 m = or3(sh<1, true>(s.A[0]), sh<1, false>(s.A[1]), sh<8, true>(s.A[2]));
     m = or3(m, sh<8, false>(s.A[3]), sh<9, true>(s.A[4]));
@@ -132,22 +113,6 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     m |= sh<7, false>(s.A[7]);
     s.reach = m;
     s.legal = andn(m, P | O);
-}
-
-// Discs flipped by a legal move at bit `mv` (board.py:161-174): walking from mv
-// along +d, the opponent run counts iff it is attached to a P disc, i.e. lies in
-// the run set of the opposite direction -d.  No bracket test needed.
-__device__ __forceinline__ u64 flips_at(u64 mv, const Position& s) {
-    const PairProp v = opaque(s.v), d9 = opaque(s.d9), d7 = opaque(s.d7);
-    u64 f = east_run(mv, opaque(s.Oi)) & s.A[1];
-    f = bfi(rev64(east_run(rev64(mv), opaque(s.rOi))), s.A[0], f);
-    f = bfi(ks<8, true>(mv, v), s.A[3], f);
-    f = bfi(ks<8, false>(mv, v), s.A[2], f);
-    f = bfi(ks<9, true>(mv, d9), s.A[5], f);
-    f = bfi(ks<9, false>(mv, d9), s.A[4], f);
-    f = bfi(ks<7, true>(mv, d7), s.A[7], f);
-    f = bfi(ks<7, false>(mv, d7), s.A[6], f);
-    return f;
 }
 
 // ---------------------------------------------------------------------------

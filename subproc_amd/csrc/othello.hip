@@ -556,6 +556,13 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
 // position (game_runner.py:169-184 records the board after Board() and after
 // every put_s), with is_game_over per position (game_recorder.py:107-114).
 // ---------------------------------------------------------------------------
+// One lane per game.  A lane's rows are its own (stride OTH_POS_STRIDE), so a
+// store instruction touches 64 different lines; positions are therefore
+// buffered kReplayBurst at a time and written back to back, so each 128-B line
+// of the board rows is completed while it is still in L2 (one row store per
+// position let half-written lines be evicted: 3.4 GB of HBM traffic per
+// 262,144-game launch against 0.64 GB written).
+constexpr int kReplayBurst = 8;
 __global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ start,
                                                         const uint8_t* __restrict__ start_turn,
                                                         const uint8_t* __restrict__ moves,
@@ -575,30 +582,54 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ 
     const u32 np = min<u32>(plies[i], OTH_MOVES_STRIDE);
     const uint8_t* mv = moves + i * OTH_MOVES_STRIDE;
     ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
-    for (u32 p = 0;; p++) {
-        out[p] = make_ulonglong2(bl, wh);
-        if (pos_turn) pos_turn[i * OTH_POS_STRIDE + p] = (uint8_t)t;
-        if (pos_end) pos_end[i * OTH_POS_STRIDE + p] = (moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0) ? 1 : 0;
-        if (p == np) break;
-        // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
-        const u32 c = mv[p];
-        if (t != OTH_BLACK && t != OTH_WHITE) continue;
-        if (c == OTH_PASS) {
-            t ^= 3u;
-        } else if (c < 64) {
-            const bool black = t == OTH_BLACK;
-            u64 P = black ? bl : wh, O = black ? wh : bl;
-            const u64 m = 1ull << c;
-            if (!((P | O) & m)) {
-                const u64 f = flips_tested(m, P, O);
-                if (f) {
-                    P |= f | m;
-                    O = andn(O, f);
-                    bl = black ? P : O;
-                    wh = black ? O : P;
-                    t ^= 3u;
+    uint8_t* out_t = pos_turn ? pos_turn + i * OTH_POS_STRIDE : nullptr;
+    uint8_t* out_e = pos_end ? pos_end + i * OTH_POS_STRIDE : nullptr;
+    for (u32 p0 = 0; p0 <= np; p0 += kReplayBurst) {
+        ulonglong2 b[kReplayBurst];
+        uint8_t tt[kReplayBurst], ee[kReplayBurst];
+        const u32 m = min<u32>(kReplayBurst, np + 1 - p0);  // positions in this burst
+#pragma unroll
+        for (u32 k = 0; k < kReplayBurst; k++) {
+            if (k < m) {
+                b[k] = make_ulonglong2(bl, wh);
+                tt[k] = (uint8_t)t;
+                ee[k] = (moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0) ? 1 : 0;
+                // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
+                const u32 p = p0 + k;
+                if (p < np && (t == OTH_BLACK || t == OTH_WHITE)) {
+                    const u32 c = mv[p];
+                    if (c == OTH_PASS) {
+                        t ^= 3u;
+                    } else if (c < 64) {
+                        const bool black = t == OTH_BLACK;
+                        u64 P = black ? bl : wh, O = black ? wh : bl;
+                        const u64 mm = 1ull << c;
+                        if (!((P | O) & mm)) {
+                            const u64 f = flips_tested(mm, P, O);
+                            if (f) {
+                                P |= f | mm;
+                                O = andn(O, f);
+                                bl = black ? P : O;
+                                wh = black ? O : P;
+                                t ^= 3u;
+                            }
+                        }
+                    }
                 }
             }
+        }
+#pragma unroll
+        for (u32 k = 0; k < kReplayBurst; k++)
+            if (k < m) out[p0 + k] = b[k];
+        if (out_t) {
+#pragma unroll
+            for (u32 k = 0; k < kReplayBurst; k++)
+                if (k < m) out_t[p0 + k] = tt[k];
+        }
+        if (out_e) {
+#pragma unroll
+            for (u32 k = 0; k < kReplayBurst; k++)
+                if (k < m) out_e[p0 + k] = ee[k];
         }
     }
 }

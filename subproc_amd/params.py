@@ -63,6 +63,20 @@ def from_learner_params(params):
     return as_weights([int(x) for x in params[1:]])
 
 
+def from_coef(coef):
+    """The learner's scaling of fitted coefficients to stored parameters
+    (progress_position_moves_learn.py:180-181, 200): per shard, coef * 127 /
+    max|coef|, then int() (truncation toward zero).  A shard whose coefficients
+    are all 0 (the learner would divide by zero) stays 0."""
+    coef = np.asarray(coef, np.float64)
+    out = np.zeros(coef.shape, np.int8)
+    for k, row in enumerate(coef):
+        mx = max(abs(float(q)) for q in row)
+        if mx > 0:
+            out[k] = [int(float(q) * (127 / mx)) for q in row]
+    return as_weights(out)
+
+
 def encode(weights, header=HEADER):
     """paramgen.write_data bytes (paramgen.py:12-19): header, the 36 weights
     as unsigned bytes (conv_num: negative -> 256 + v), trailing 0."""

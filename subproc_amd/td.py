@@ -20,13 +20,18 @@ Here the whole batch runs on the device:
      Python learner's;
   4. the result is merged into the device-resident, key-sorted table.
 Batches applied one after another equal one batch of all their books.
-Redis/sampling/regression stay out of scope; values are kept as float64 (the
-Python learner's float, before any store round trip).
+Values are kept as float64 (the Python learner's float, before any store
+round trip).  ``StateMap.fit`` runs the learner's regression step
+(fit_parameter, progress_position_moves_learn.py:160-184) over every state of
+a shard on the device instead of a random 50,000-state sample; Redis and the
+pyres fan-out stay out of scope.
 """
+import numpy as np
 import torch
 
 from . import _lib
 from ._lib import POS_STRIDE, check
+from .params import SHARDS
 
 A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
 LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
@@ -52,6 +57,12 @@ def counts_to_key(c):
 def key_to_counts(k):
     k = int(k)
     return tuple((k >> s) & ((1 << w) - 1) for s, w in zip(_SHIFTS, _WIDTH))
+
+
+def unpack_counts(keys):
+    """Packed keys (device int64 tensor) -> (n, 10) int64 counts() tuples."""
+    cols = [(keys >> s) & ((1 << w) - 1) for s, w in zip(_SHIFTS, _WIDTH)]
+    return torch.stack(cols, 1)
 
 
 def hash_string(k):
@@ -161,3 +172,30 @@ class StateMap:
     def items(self):
         """{hash_from_book string: value} on the host."""
         return {hash_string(k): v for k, v in zip(self.keys.cpu().tolist(), self.values.cpu().tolist())}
+
+    def fit(self, shards=SHARDS):
+        """The learner's per-shard regression (fit_parameter,
+        progress_position_moves_learn.py:160-184: LinearRegression with an
+        intercept of the state value on counts()[1:], states whose counts()[0]
+        lies in the shard) over EVERY state of the map, not a random sample.
+        Normal equations of the centred data, accumulated in float64 on the
+        device, solved (minimum norm) on the host.  Returns float64 arrays
+        coef (len(shards), 9), intercept (len(shards),), n (len(shards),)."""
+        c = unpack_counts(self.keys)
+        phase, X = c[:, 0], c[:, 1:].double()
+        coef = np.zeros((len(shards), X.shape[1]))
+        icpt = np.zeros(len(shards))
+        nk = np.zeros(len(shards), np.int64)
+        for k, (lo, hi) in enumerate(shards):
+            m = (phase >= lo) & (phase <= hi)
+            Xk, yk = X[m], self.values[m]
+            nk[k] = Xk.shape[0]
+            if nk[k] == 0:
+                continue
+            xm, ym = Xk.mean(0), yk.mean()
+            Xc = Xk - xm
+            A = (Xc.T @ Xc).cpu().numpy()
+            b = (Xc.T @ (yk - ym)).cpu().numpy()
+            coef[k] = np.linalg.lstsq(A, b, rcond=None)[0]
+            icpt[k] = float(ym) - float(xm.cpu().numpy() @ coef[k])
+        return coef, icpt, nk

@@ -78,3 +78,22 @@ def test_td_ema_zero_states_in_long_segments():
     _lib.check(lib.oth_td_ema(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(), len(lengths),
                               torch.cuda.current_stream().cuda_stream), "oth_td_ema")
     assert out.cpu().tolist() == [w[1] for w in want]
+
+
+def test_fit_on_device_matches_sklearn():
+    from sklearn import linear_model
+    from subproc_amd import params
+
+    r = ops.rollout(8192, 23, 0, "random", record_moves=True, device=DEV)
+    sm = td.StateMap(DEV)
+    sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
+    coef, icpt, n = sm.fit()
+    c = td.unpack_counts(sm.keys).cpu().numpy()
+    y = sm.values.cpu().numpy()
+    for k, (lo, hi) in enumerate(td.SHARDS):
+        m = (c[:, 0] >= lo) & (c[:, 0] <= hi)
+        assert m.sum() == n[k]
+        lr = linear_model.LinearRegression(fit_intercept=True).fit(c[m, 1:].astype(np.float64), y[m])
+        np.testing.assert_allclose(coef[k], lr.coef_, rtol=1e-6, atol=1e-9)  # float64 normal equations vs SVD
+    w = params.from_coef(coef)
+    assert w.dtype == np.int8 and np.abs(w).max() == 127

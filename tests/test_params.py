@@ -49,3 +49,16 @@ def test_shards_and_validation():
         params.as_weights(np.full((4, 9), 200))
     with pytest.raises(ValueError):
         params.decode(b"\x02" + bytes(36) + b"\x01")
+
+
+def test_from_coef_is_the_learners_scaling():
+    coef = np.array([[0.5, -2.0, 0.25, 0.0, 1.0, -1.0, 0.125, 1.999, -0.001],
+                     [0.0] * 9,
+                     [3.0, 1.5, -3.0, 0.3, 0.1, 2.9, -2.9, 1.0, 0.01],
+                     [1e-3, 2e-3, -4e-3, 0, 0, 0, 0, 0, 1e-3]])
+    got = params.from_coef(coef)
+    for k, row in enumerate(coef):
+        mx = max(abs(q) for q in row)
+        want = [int(q * (127 / mx)) for q in row] if mx else [0] * 9  # coef = 127/max|coef|; int(i*coef)
+        assert got[k].tolist() == want
+    assert got[0][1] == -127 and got[2][0] == 127

@@ -70,3 +70,29 @@ def test_cpu_abi_td_matches_fixture_and_batches_compose():
     assert run(boards, plies, {}) == want
     s = run(boards[:100], plies[:100], {})
     assert run(boards[100:], plies[100:], s) == want
+
+
+def test_fit_matches_sklearn_on_fixture_states():
+    """StateMap.fit == sklearn LinearRegression(fit_intercept=True) per shard
+    (fit_parameter, progress_position_moves_learn.py:160-184) on the same
+    states; float64, tolerance rtol 1e-6 / atol 1e-9 on the coefficients."""
+    import torch
+    from sklearn import linear_model
+
+    f = fixture()
+    sm = td.StateMap("cpu")
+    keys = sorted(td.counts_to_key(k) for k in f)
+    sm.keys = torch.tensor(keys, dtype=torch.int64)
+    sm.values = torch.tensor([f[td.key_to_counts(k)] for k in keys], dtype=torch.float64)
+    coef, icpt, n = sm.fit()
+    assert n.sum() == len(keys)
+    for k, (lo, hi) in enumerate(td.SHARDS):
+        rows = [(c, v) for c, v in f.items() if lo <= c[0] <= hi]
+        assert len(rows) == n[k]
+        if len(rows) < 2:
+            continue
+        X = np.array([c[1:] for c, _ in rows], np.float64)
+        y = np.array([v for _, v in rows])
+        lr = linear_model.LinearRegression(fit_intercept=True).fit(X, y)
+        np.testing.assert_allclose(coef[k], lr.coef_, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(icpt[k], lr.intercept_, rtol=1e-6, atol=1e-9)

@@ -113,6 +113,15 @@ int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t 
                      int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
                      uint8_t* moves, int64_t* hist, int64_t n, void* stream);
 
+/* A match between two eval tables (the GPU counterpart of GameRunner playing
+ * engine A as Black against engine B as White, game_runner.py:154-201): as
+ * oth_rollout_eval, but Black's moves use weights_black and White's moves
+ * weights_white (both HOST pointers to OTH_EVAL_WEIGHTS int8, copied into the
+ * launch).  oth_rollout_eval(w) == oth_rollout_match(w, w). */
+int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                      int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+
 /* Synthetic reachable mid-game positions for the step benchmark (config 2):
  * position index0+j is a random-policy playout of 10..49 plies from the opening
  * at which the mover has >= 1 legal move, plus that mover's random legal move

@@ -55,7 +55,7 @@ def lib():
         L.oracle_legal.argtypes = [P, P, P, I64]
         L.oracle_step.argtypes = [P, P, P, P, P, P, P, P, P, I64]
         L.oracle_result.argtypes = [P, P, P, P, P, I64]
-        L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I, P]
+        L.oracle_rollout.argtypes = [P, P, U64, U64, I, I, P, P, P, P, P, I64, I, P, P]
         L.oracle_sample_midgame.argtypes = [U64, U64, P, P, P, P, I64]
         L.oracle_features.argtypes = [P, P, P, I64]
         L.oracle_eval.argtypes = [P, P, P, P, I64]
@@ -128,9 +128,11 @@ def _weights(w):
 
 
 def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=None, record_moves=False,
-            n_threads=0, weights=None):
-    """policy 0 random, 1 greedy, 2 eval (weights: 36 int8, [shard][feature])."""
+            n_threads=0, weights=None, weights_white=None):
+    """policy 0 random, 1 greedy, 2 eval (weights: 36 int8, [shard][feature];
+    weights_white: White's table in a match, default = weights)."""
     w = None if weights is None else _weights(weights)
+    ww = None if weights_white is None else _weights(weights_white)
     if policy == 2 and w is None:
         raise ValueError("policy 2 (eval) needs weights")
     start = None if start is None else _boards(start)
@@ -141,7 +143,7 @@ def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=N
     mv = np.empty((n, MOVES_STRIDE), np.uint8) if record_moves else None
     h = np.zeros(HIST_BINS, np.int64)
     lib().oracle_rollout(_p(start), _p(st), seed, game_id0, policy, n_random, _p(fb), _p(d), _p(pl), _p(mv), _p(h),
-                         n, n_threads, _p(w))
+                         n, n_threads, _p(w), _p(ww))
     return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h)
 
 

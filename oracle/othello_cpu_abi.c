@@ -26,7 +26,7 @@ int oracle_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, in
                   int64_t n);
 int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
-                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights);
+                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights, const int8_t* weights_white);
 int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
                           uint8_t* move, int64_t n);
 int oracle_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n);
@@ -70,7 +70,7 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
     if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return oracle_rollout(start, start_turn, seed, game_id0, policy, n_random, final_boards, diff, plies, moves, hist,
-                          n, 0, NULL);
+                          n, 0, NULL, NULL);
 }
 
 int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
@@ -80,7 +80,17 @@ int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t 
     if (n < 0 || !weights) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return oracle_rollout(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, final_boards, diff, plies,
-                          moves, hist, n, 0, weights);
+                          moves, hist, n, 0, weights, NULL);
+}
+
+int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                      int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || !weights_black || !weights_white) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return oracle_rollout(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, final_boards, diff, plies,
+                          moves, hist, n, 0, weights_black, weights_white);
 }
 
 int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,

@@ -286,7 +286,8 @@ static int eval_of(const Board* s, int t, const int8_t* w) {
 
 /* One game to terminal from s, game_runner.py:165-201 loop with the build's
  * policies: a side with no move passes ('PS'). */
-static int play_game(Board* s, uint64_t key, int policy, int n_random, const int8_t* w, uint8_t* moves) {
+static int play_game(Board* s, uint64_t key, int policy, int n_random, const int8_t* w, const int8_t* w_white,
+                     uint8_t* moves) {
     int ply = 0;
     GameRng rng = rng_init(key);
     while (!is_game_over(s)) {
@@ -312,7 +313,7 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, const int
                 if (!(legal >> sq & 1)) continue;
                 Board c = *s;
                 put_code(&c, sq);
-                int v = eval_of(&c, s->turn, w);
+                int v = eval_of(&c, s->turn, s->turn == White ? w_white : w);
                 if (v > bestv) { bestv = v; best = sq; }
             }
             code = best;
@@ -325,11 +326,13 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, const int
     return ply;
 }
 
-/* policy 0 random, 1 greedy, 2 eval (weights: int8[36], used by policy 2 only) */
+/* policy 0 random, 1 greedy, 2 eval (weights: int8[36], used by policy 2 only;
+ * weights_white NULL = White uses `weights` too, else White's table: a match) */
 int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
-                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights) {
+                   int64_t* hist, int64_t n, int n_threads, const int8_t* weights, const int8_t* weights_white) {
     if (policy == 2 && !weights) return -1;
+    if (!weights_white) weights_white = weights;
     uint64_t S = seed_state(seed);
     int64_t h[HIST_BINS];
     memset(h, 0, sizeof h);
@@ -346,7 +349,7 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
             if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
             else board_init(&s);
             if (moves) memset(moves + i * MOVES_STRIDE, 255, MOVES_STRIDE);
-            int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random, weights,
+            int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random, weights, weights_white,
                               moves ? moves + i * MOVES_STRIDE : 0);
             int d = n_of(&s, Black) - n_of(&s, White);
             uint64_t bl, wh;

@@ -72,6 +72,7 @@ __constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull
 // (d - 1) >> 4 for d in 1..64 (shards 0..16, 17..32, 33..48, 49..64 of
 // progress_position_moves_learn.py:112-113).
 constexpr int kEvalRow = 12;
+constexpr int kEvalTable = OTH_EVAL_PHASES * kEvalRow;
 struct EvalWeights {
     int8_t w[OTH_EVAL_WEIGHTS];
 };
@@ -96,13 +97,13 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // first in puttables order).  A child's score is a key whose minimum is the
 // choice: (score << 6) | square.
 template <int POLICY>
-__device__ __forceinline__ u32 child_key(u64 P, u64 O, const Position& s, u32 sq, const u64* rays, const int* w_s) {
+__device__ __forceinline__ u32 child_key(u64 P, u64 O, const Position& s, u32 sq, const u64* rays, const int* w_tab) {
     const u64 mv = 1ull << sq;
     const u64 f = flips_rays(sq, mv, s, rays);
     const u64 P2 = P | f | mv, O2 = andn(O, f);
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
     // every child has popcount(P|O) + 1 discs: one weight row per parent
-    const int* row = w_s + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
+    const int* row = w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
@@ -110,15 +111,15 @@ __device__ __forceinline__ u32 child_key(u64 P, u64 O, const Position& s, u32 sq
     return ((u32)((1 << 20) - v) << 6) | sq;
 }
 
-// one lane alone over its own children
+// one lane alone over its own children (w_tab: the mover's eval table)
 template <int POLICY>
-__device__ __forceinline__ u32 lane_choose(const Position& s, u64 P, u64 O, const u64* rays, const int* w_s) {
+__device__ __forceinline__ u32 lane_choose(const Position& s, u64 P, u64 O, const u64* rays, const int* w_tab) {
     u32 best = 0xFFFFFFFFu;
     u64 legal = s.legal;
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         legal &= legal - 1;
-        best = min(best, child_key<POLICY>(P, O, s, sq, rays, w_s));
+        best = min(best, child_key<POLICY>(P, O, s, sq, rays, w_tab));
     }
     return best & 63u;
 }
@@ -134,7 +135,7 @@ __device__ __forceinline__ u32 lane_choose(const Position& s, u64 P, u64 O, cons
 constexpr int kCoopCap = 64 * 20;  // children per wave per ply (mean mobility ~8.4)
 struct CoopWave {
     u64 rec[64][10];          // parent lane: P, O, run sets A[0..7]
-    uint16_t list[kCoopCap];  // (parent lane << 8) | square
+    uint16_t list[kCoopCap];  // (parent lane << 8) | (parent plays White) << 6 | square
     u32 best[64];
     u32 total;
 };
@@ -150,8 +151,9 @@ __device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, Positi
     s.Oi = O & INNER_FILES;
     s.rOi = rev64(s.Oi);
 }
+// w_s: the two eval tables (Black's, then White's, kEvalTable ints each)
 template <int POLICY>
-__device__ u32 coop_choose(bool need, u64 P, u64 O, const Position& pos, CoopWave& cw, const u64* rays,
+__device__ u32 coop_choose(bool need, u64 P, u64 O, u32 side, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, u32 lane) {
     if (need) {
         u64* r = cw.rec[lane];
@@ -163,9 +165,10 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, const Position& pos, CoopWav
         const u32 cnt = (u32)__popcll(pos.legal);
         u32 off = atomicAdd(&cw.total, cnt);
         if (off + cnt <= (u32)kCoopCap) {
+            const u32 tag = (lane << 8) | (side == OTH_WHITE ? 64u : 0u);
             u64 m = pos.legal;
             while (m) {
-                cw.list[off++] = (uint16_t)((lane << 8) | ((u32)__ffsll((unsigned long long)m) - 1u));
+                cw.list[off++] = (uint16_t)(tag | ((u32)__ffsll((unsigned long long)m) - 1u));
                 m &= m - 1;
             }
         }
@@ -174,7 +177,7 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, const Position& pos, CoopWav
     const u32 total = __builtin_amdgcn_readfirstlane(cw.total);
     u32 result = 64;
     if (total > (u32)kCoopCap) {
-        if (need) result = lane_choose<POLICY>(pos, P, O, rays, w_s);
+        if (need) result = lane_choose<POLICY>(pos, P, O, rays, w_s + (side == OTH_WHITE ? kEvalTable : 0));
     } else {
         const u32 rounds = (total + 63u) >> 6;
         for (u32 k = 0; k < rounds; k++) {
@@ -185,7 +188,8 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, const Position& pos, CoopWav
                 u64 Pp, Op;
                 Position ps;
                 load_parent(cw.rec[par], Pp, Op, ps);
-                atomicMin(&cw.best[par], child_key<POLICY>(Pp, Op, ps, e & 63u, rays, w_s));
+                atomicMin(&cw.best[par],
+                          child_key<POLICY>(Pp, Op, ps, e & 63u, rays, w_s + ((e & 64u) ? kEvalTable : 0)));
             }
         }
         wave_sync();
@@ -314,7 +318,7 @@ struct RolloutArgs {
     long long* hist;
     int64_t n;
     unsigned long long* work;  // batch counter, zeroed before the launch
-    EvalWeights ew;            // OTH_POLICY_EVAL only
+    EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table
 };
 
 #ifdef OTH_DIAG
@@ -331,13 +335,16 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
     __shared__ u64 rays[kRayRows * 64];
-    __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? OTH_EVAL_PHASES * kEvalRow : 1];
+    __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
     if (POLICY != OTH_POLICY_RANDOM && threadIdx.x < kBlock / 64) coop[threadIdx.x].total = 0;
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
-    if (POLICY == OTH_POLICY_EVAL) eval_weights_to_lds(a.ew, w_s);
+    if (POLICY == OTH_POLICY_EVAL) {
+        eval_weights_to_lds(a.ew[0], w_s);
+        eval_weights_to_lds(a.ew[1], w_s + kEvalTable);
+    }
     __syncthreads();
 
     const int lane = lane_id();
@@ -468,7 +475,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     }
                 }
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
-                    const u32 c = coop_choose<POLICY>(choose, P, O, pos, coop[threadIdx.x >> 6], rays, w_s,
+                    const u32 c = coop_choose<POLICY>(choose, P, O, side, pos, coop[threadIdx.x >> 6], rays, w_s,
                                                       (u32)lane);
                     if (choose) sq = c;
                 }
@@ -935,8 +942,8 @@ int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_
 
 namespace {
 int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
-                   int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
-                   uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+                   int n_random, const int8_t* w_black, const int8_t* w_white, uint64_t* final_boards, int8_t* diff,
+                   uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
     RolloutArgs a;
     a.start = start;
     a.start_turn = start_turn;
@@ -950,7 +957,10 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     a.moves = moves;
     a.hist = (long long*)hist;
     a.n = n;
-    for (int k = 0; k < OTH_EVAL_WEIGHTS; k++) a.ew.w[k] = weights ? weights[k] : 0;
+    for (int k = 0; k < OTH_EVAL_WEIGHTS; k++) {
+        a.ew[0].w[k] = w_black ? w_black[k] : 0;
+        a.ew[1].w[k] = w_white ? w_white[k] : 0;
+    }
     const DeviceState* ds = device_state();
     if (!ds) return status(hipErrorInvalidDevice);
     const Tuning& t = ds->tuning;
@@ -980,8 +990,8 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
                 int64_t n, void* stream) {
     if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    return rollout_launch(start, start_turn, seed, game_id0, policy, n_random, nullptr, final_boards, diff, plies,
-                          moves, hist, n, stream);
+    return rollout_launch(start, start_turn, seed, game_id0, policy, n_random, nullptr, nullptr, final_boards, diff,
+                          plies, moves, hist, n, stream);
 }
 
 int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
@@ -989,8 +999,17 @@ int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t 
                      uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
     if (n < 0 || !weights) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights, final_boards, diff,
-                          plies, moves, hist, n, stream);
+    return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights, weights, final_boards,
+                          diff, plies, moves, hist, n, stream);
+}
+
+int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                      int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+    if (n < 0 || !weights_black || !weights_white) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights_black, weights_white,
+                          final_boards, diff, plies, moves, hist, n, stream);
 }
 
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,

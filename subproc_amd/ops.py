@@ -148,7 +148,8 @@ def result(boards):
 
 
 def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start_turn=None, record_moves=False,
-            hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True, weights=None):
+            hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True, weights=None,
+            weights_white=None):
     """Play n games to terminal on the GPU (one lane per game).
 
     Game i uses the RNG stream of global id game_id0 + i, so results do not
@@ -159,7 +160,9 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
 
     Policies: "random"; "greedy" (minimise the opponent's mobility) and "eval"
     (maximise the mover's linear eval under ``weights``, int8 [4, 9], default
-    params.DEFAULT_WEIGHTS) after ``n_random`` random plies.
+    params.DEFAULT_WEIGHTS) after ``n_random`` random plies.  With
+    ``weights_white`` the eval policy is a match: Black plays ``weights``,
+    White plays ``weights_white`` (oth_rollout_match).
     """
     if policy not in _POLICIES:
         raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
@@ -182,12 +185,16 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
         return None if t is None else t.data_ptr()
 
     with torch.cuda.device(d):
-        if _POLICIES[policy] == POLICY_EVAL:
+        if _POLICIES[policy] == POLICY_EVAL and weights_white is not None:
+            check(_lib.load().oth_rollout_match(ps, pst, seed & (2**64 - 1), game_id0, n_random,
+                                                _weights_ptr(weights), _weights_ptr(weights_white), ptr(fb), ptr(df),
+                                                ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout_match")
+        elif _POLICIES[policy] == POLICY_EVAL:
             check(_lib.load().oth_rollout_eval(ps, pst, seed & (2**64 - 1), game_id0, n_random, _weights_ptr(weights),
                                                ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()),
                   "oth_rollout_eval")
         else:
-            if weights is not None:
+            if weights is not None or weights_white is not None:
                 raise ValueError("weights apply to policy 'eval' only")
             check(_lib.load().oth_rollout(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy], n_random,
                                           ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout")

@@ -196,6 +196,7 @@ def play(args):
     """
     seed, g, policy, n_random, bl, wh, turn = args[:7]
     weights = args[7] if len(args) > 7 else None
+    weights_white = args[8] if len(args) > 8 and args[8] is not None else weights  # a match: White's table
     rng = GameRng(game_key(seed_state(seed), g))
     b = from_bits(bl, wh, turn)
     moves = []
@@ -221,7 +222,7 @@ def play(args):
             for (x, y) in puts:
                 c = clone(b)
                 assert c.put_s(c.handstr_from_coord(x, y)) > 0
-                v = eval_value(c, "O" if b.turn == Black else "X", weights)
+                v = eval_value(c, "O" if b.turn == Black else "X", weights if b.turn == Black else weights_white)
                 if bestv is None or v > bestv:
                     best, bestv = x + 8 * y, v
             code = best
@@ -406,10 +407,11 @@ def main():
     )
 
     # ---------------------------------------------------------------- rollouts
-    def rollouts(name, seed, g0, n, policy, n_random, starts=None, weights=None):
+    def rollouts(name, seed, g0, n, policy, n_random, starts=None, weights=None, weights_white=None):
         if starts is None:
             starts = [(ib, iw, Black)] * n
-        args = [(seed, g0 + i, policy, n_random, s[0], s[1], s[2], weights) for i, s in enumerate(starts)]
+        args = [(seed, g0 + i, policy, n_random, s[0], s[1], s[2], weights, weights_white)
+                for i, s in enumerate(starts)]
         res = pool.map(play, args, chunksize=4)
         mv = np.full((n, 128), 255, np.uint8)
         for i, r in enumerate(res):
@@ -422,7 +424,8 @@ def main():
             start_turn=np.array([s[2] for s in starts], np.uint8),
             moves=mv, final_black=u64([r[1] for r in res]), final_white=u64([r[2] for r in res]),
             diff=np.array([r[3] for r in res], np.int8), plies=np.array([r[4] for r in res], np.uint8),
-            **({} if weights is None else {"weights": np.array(weights, np.int8)}))
+            **({} if weights is None else {"weights": np.array(weights, np.int8)}),
+            **({} if weights_white is None else {"weights_white": np.array(weights_white, np.int8)}))
 
     rollouts("rollout_random", SEED, 0, 256, 0, 0)
     rollouts("rollout_random_offset", 12345, (1 << 20) * 3 + 77, 128, 0, 0)
@@ -437,6 +440,8 @@ def main():
     wrand = np.random.default_rng(77).integers(-127, 128, (4, 9)).tolist()
     rollouts("rollout_eval", SEED, 0, 128, 2, 10, weights=wdef)
     rollouts("rollout_eval_rand_from_mid", 4242, 77, 64, 2, 0, starts=mid[:64], weights=wrand)
+    # a match: the reference's default table as Black against the random table as White
+    rollouts("rollout_match", 5150, 9, 128, 2, 6, weights=wdef, weights_white=wrand)
     boards = [from_bits(p[0], p[1], p[2]) for p in pos[:512]]
     np.savez_compressed(
         os.path.join(OUT, "eval_values.npz"),

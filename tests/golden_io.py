@@ -23,4 +23,4 @@ def h(x):
 
 
 ROLLOUT_FIXTURES = ["rollout_random", "rollout_random_offset", "rollout_random_from_mid", "rollout_greedy",
-                    "rollout_greedy_from_mid", "rollout_eval", "rollout_eval_rand_from_mid"]
+                    "rollout_greedy_from_mid", "rollout_eval", "rollout_eval_rand_from_mid", "rollout_match"]

@@ -78,7 +78,12 @@ def test_rollout_fixtures(name):
     stt = z["start_turn"] if from_mid else None
     fb, df, pl = np.empty((n, 2), np.uint64), np.empty(n, np.int8), np.empty(n, np.uint8)
     mv, hist = np.empty((n, _lib.MOVES_STRIDE), np.uint8), np.zeros(_lib.HIST_BINS, np.int64)
-    if int(z["policy"]) == 2:
+    if "weights_white" in z:
+        w = np.ascontiguousarray(z["weights"].reshape(-1), np.int8)
+        ww = np.ascontiguousarray(z["weights_white"].reshape(-1), np.int8)
+        rc = lib().oth_rollout_match(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["n_random"]), P(w),
+                                     P(ww), P(fb), P(df), P(pl), P(mv), P(hist), n, None)
+    elif int(z["policy"]) == 2:
         w = np.ascontiguousarray(z["weights"].reshape(-1), np.int8)
         rc = lib().oth_rollout_eval(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["n_random"]), P(w),
                                     P(fb), P(df), P(pl), P(mv), P(hist), n, None)

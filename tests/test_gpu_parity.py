@@ -150,7 +150,7 @@ def test_rollout_fixtures(name):
     r = ops.rollout(n, int(z["seed"]), int(z["game_id0"]), policy, int(z["n_random"]),
                     start=B(z["start_black"], z["start_white"]) if from_mid else None,
                     start_turn=T(z["start_turn"]) if from_mid else None, record_moves=True, device=DEV,
-                    weights=z.get("weights"))
+                    weights=z.get("weights"), weights_white=z.get("weights_white"))
     np.testing.assert_array_equal(r.moves.cpu().numpy(), z["moves"])
     np.testing.assert_array_equal(r.plies.cpu().numpy(), z["plies"])
     np.testing.assert_array_equal(r.diff.cpu().numpy(), z["diff"])
@@ -325,3 +325,17 @@ def test_config4_global_histogram_equals_shards():
         ops.rollout(n, 0x5EED, r * n, hist=acc, device=DEV, want_boards=False, want_diff=False, want_plies=False)
     assert torch.equal(acc, whole.hist)
     assert int(whole.hist[:129].sum()) == 8 * n
+
+
+def test_rollout_match_vs_oracle_and_equal_tables():
+    from subproc_amd.params import DEFAULT_WEIGHTS
+    n = 4096
+    wr = np.random.default_rng(8).integers(-127, 128, (4, 9)).astype(np.int8)
+    r = ops.rollout(n, 44, 1 << 22, "eval", 8, weights=DEFAULT_WEIGHTS, weights_white=wr, device=DEV)
+    o = oracle.rollout(n, 44, 1 << 22, policy=2, n_random=8, weights=DEFAULT_WEIGHTS, weights_white=wr)
+    assert (U(r.final_boards) == o["final_boards"]).all()
+    assert (r.hist.cpu().numpy() == o["hist"]).all()
+    # a match of a table against itself is the plain eval policy
+    a = ops.rollout(n, 45, 0, "eval", 10, weights=wr, weights_white=wr, record_moves=True, device=DEV)
+    b = ops.rollout(n, 45, 0, "eval", 10, weights=wr, record_moves=True, device=DEV)
+    assert torch.equal(a.moves, b.moves) and torch.equal(a.hist, b.hist)

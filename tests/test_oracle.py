@@ -76,7 +76,7 @@ def test_rollouts(name):
     r = oracle.rollout(n, int(z["seed"]), int(z["game_id0"]), int(z["policy"]), int(z["n_random"]),
                        start=np.stack([z["start_black"], z["start_white"]], 1) if from_mid else None,
                        start_turn=z["start_turn"] if from_mid else None, record_moves=True,
-                       weights=z.get("weights"))
+                       weights=z.get("weights"), weights_white=z.get("weights_white"))
     np.testing.assert_array_equal(r["moves"], z["moves"])
     np.testing.assert_array_equal(r["plies"], z["plies"])
     np.testing.assert_array_equal(r["diff"], z["diff"])

@@ -38,6 +38,14 @@ def main():
               % (r, games, dt * 1e3, n_upd, len(sm), s["black_win_rate"], s["avg_diff"]))
         print("  weights by shard:", [list(map(int, row)) for row in w_new])
         w = w_new
+    # the learned table against the learner's default one, both colour assignments
+    # (oth_rollout_match: the GPU counterpart of GameRunner's engine A vs engine B)
+    for name, wb, ww in (("learned(B) vs default(W)", w, params.DEFAULT_WEIGHTS),
+                         ("default(B) vs learned(W)", params.DEFAULT_WEIGHTS, w)):
+        m = ops.rollout(games, 99, 1 << 40, "eval", 10, weights=wb, weights_white=ww, device=dev)
+        s = dist.hist_summary(m.hist)
+        print("match %s: black wins %.3f, white wins %.3f, draws %.3f" %
+              (name, s["black_win_rate"], s["white_win_rate"], int(m.hist[131]) / s["games"]))
 
 
 if __name__ == "__main__":

@@ -339,3 +339,38 @@ def test_rollout_match_vs_oracle_and_equal_tables():
     a = ops.rollout(n, 45, 0, "eval", 10, weights=wr, weights_white=wr, record_moves=True, device=DEV)
     b = ops.rollout(n, 45, 0, "eval", 10, weights=wr, record_moves=True, device=DEV)
     assert torch.equal(a.moves, b.moves) and torch.equal(a.hist, b.hist)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 1000])
+def test_rollout_ragged_sizes_vs_oracle(n):
+    for policy, pid in (("random", 0), ("greedy", 1)):
+        r = ops.rollout(n, 31, 7, policy, 10, record_moves=True, device=DEV)
+        o = oracle.rollout(n, 31, 7, policy=pid, n_random=10, record_moves=True)
+        assert (r.moves.cpu().numpy() == o["moves"]).all(), (n, policy)
+        assert (r.hist.cpu().numpy() == o["hist"]).all(), (n, policy)
+
+
+def test_rollout_game_ids_wrap_2_64():
+    """Game ids are u64 and wrap (game i uses id game_id0 + i mod 2^64)."""
+    g0 = 2**64 - 10
+    r = ops.rollout(32, 5, g0, device=DEV, record_moves=True)
+    o = oracle.rollout(32, 5, g0, record_moves=True)
+    assert (r.moves.cpu().numpy() == o["moves"]).all()
+    tail = ops.rollout(22, 5, 0, device=DEV, record_moves=True)  # ids 0..21 == games 10..31 above
+    assert torch.equal(tail.moves, r.moves[10:])
+
+
+def test_concurrent_rollouts_on_two_streams():
+    """Launches in flight together use separate work counters (g_work slots):
+    results equal the same launches run one after the other."""
+    n = 1 << 18
+    seq = [ops.rollout(n, 77, k * n, "random", device=DEV) for k in range(2)]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for k, st in enumerate((s1, s2)):
+        with torch.cuda.stream(st):
+            outs.append(ops.rollout(n, 77, k * n, "random", device=DEV))
+    torch.cuda.synchronize()
+    for a, b in zip(seq, outs):
+        assert torch.equal(a.final_boards, b.final_boards) and torch.equal(a.hist, b.hist)

@@ -1,11 +1,15 @@
 // othello.hip — MI355X (gfx950) kernels + C-ABI for the batched Othello env.
 //
 // Replaces the step path of ysnrkdm/subproc board.py:
-//   puttables / n_puttable_for  (board.py:46-55)   -> moves()      Kogge-Stone fills
-//   put / put_s                 (board.py:161-209) -> flips()      Kogge-Stone fills
+//   puttables / n_puttable_for  (board.py:46-55)   -> moves(): Kogge-Stone fills + carry rays
+//   put / put_s                 (board.py:161-209) -> step: flips_tested; rollouts: flips_rays
+//                                                     (LDS ray table + run-set prefix)
 //   is_game_over                (board.py:57-58)   -> two-pass rule in the rollout loop
 //   n_black / n_white + result  (board.py:37-41, game_runner.py:194-199)
 //   play loop                   (game_runner.py:165-201) -> rollout_kernel
+// and the §8f rows beside it: replay + book text (game_recorder.py), counts()
+// features, the learner's linear eval, eval-table self-play / matches, and the
+// TD state-map update (progress_position_moves_learn.py:37-62).
 //
 // Design: one game per lane, state in VGPRs as two uint64 bitboards
 // (mover P, opponent O); pure integer/bitwise VALU work, no MFMA.  The cost of
@@ -13,8 +17,9 @@
 // rollout kernel keeps per-iteration control flow minimal: a wave dequeues 64
 // game ids (one per lane) from a per-launch counter, plays them out with
 // __ballot-driven lane masking, then dequeues again.  LDS holds the k-th-bit
-// byte table and the per-workgroup win/score histogram (one global atomic per
-// non-zero bin per workgroup at exit).
+// byte table, the ray table, the per-workgroup win/score histogram (one global
+// atomic per non-zero bin per workgroup at exit) and, for the 1-ply policies,
+// the per-wave cooperative child list (coop_choose).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -309,7 +314,6 @@ struct RolloutArgs {
     const uint8_t* start_turn;
     u64 seed_state;
     u64 game_id0;
-    int policy;
     int n_random;
     u64* final_boards;
     int8_t* diff;
@@ -949,7 +953,6 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     a.start_turn = start_turn;
     a.seed_state = mix64(seed + GOLDEN64);
     a.game_id0 = game_id0;
-    a.policy = policy;
     a.n_random = n_random;
     a.final_boards = final_boards;
     a.diff = diff;

@@ -71,7 +71,8 @@ def parse():
     p.add_argument("--games", type=int, default=1 << 20, help="games per GPU per bench step (rollout workloads)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--no-secondary", action="store_true", help="skip the secondary step/greedy/cpu measurements")
-    p.add_argument("--cpu-games", type=int, default=100000, help="bounded cpu_baseline sample (games)")
+    p.add_argument("--cpu-games", type=int, default=250000,
+                   help="bounded cpu_baseline sample (games): ~20 s of CPU work on 16 host threads")
     p.add_argument("--allreduce", choices=["async", "sync", "end"], default="end",
                    help="histogram all-reduce at N>1: per step overlapped with the next step (async), "
                         "per step blocking (sync), or once over all timed steps (end)")

@@ -14,6 +14,8 @@ Also reported on rank 0 (secondary, same JSON line):
   * step_65536 : config 2, one oth_step launch over 65,536 reachable mid-game
     positions (52 algorithmic HBM bytes per step), repeated launches;
   * step_steady: the same kernel over 16,777,216 positions (HBM roofline);
+  * rollout_16M: the config-3 kernel on 16,777,216 games per launch (the
+    per-launch tail amortised: the kernel's steady-state rate);
   * greedy     : config 5, 1,048,576 1-ply greedy-mobility games;
   * eval       : 1,048,576 games of the 1-ply linear-eval policy with the
     learner's default weights (SURVEY.md §8f row 2);
@@ -214,6 +216,8 @@ def main():
                                             lambda x: x, launches=200)
             sec["step_steady_16M"] = _bench_step(ops, torch, dev, stream, args, 1 << 24, 1, torch.cuda.synchronize,
                                                  lambda x: x, launches=10)
+        if args.workload == "rollout":
+            sec["rollout_16M"] = _bench_rollout_big(ops, torch, dev, args)
         if args.workload != "greedy":
             sec["greedy_1M"] = _bench_greedy(ops, torch, dev, stream, args)
         sec["eval_1M"] = _bench_greedy(ops, torch, dev, stream, args, policy="eval")
@@ -266,6 +270,25 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
         r["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s", "frac": va / VALU_PEAK_WINSTR,
                      "busy_pmc": prof.get("valu_busy")}
     return r
+
+
+def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):
+    """The config-3 kernel on 16,777,216 games per launch: the per-launch tail
+    (the last batches of 64 games start late and run ~60 plies) amortises, so
+    this shows the kernel's steady-state rate next to config 3's 1M batch."""
+    hist = torch.zeros(133, dtype=torch.int64, device=dev)
+    ops.rollout(games, args.seed, 1 << 42, "random", hist=hist, device=dev, want_boards=False, want_diff=False,
+                want_plies=False)
+    torch.cuda.synchronize()
+    hist.zero_()
+    t0 = time.perf_counter()
+    for k in range(reps):
+        ops.rollout(games, args.seed, (1 << 42) + (k + 1) * games, "random", hist=hist, device=dev,
+                    want_boards=False, want_diff=False, want_plies=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "env-steps/sec (random self-play, 16M games per launch)", "value": int(hist[132]) / dt,
+            "unit": "env-steps/s", "games": games, "launches": reps, "ms_per_launch": dt / reps * 1e3}
 
 
 def _bench_greedy(ops, torch, dev, stream, args, policy="greedy"):

@@ -361,6 +361,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
         if (lane == 0) base = atomicAdd(a.work, 64ull);
         base = __shfl(base, 0);
         if (base >= n) break;  // wave-uniform
+
         const u64 g = base + lane;
         bool active = g < n;
         u64 P = OPEN_BLACK, O = OPEN_WHITE;

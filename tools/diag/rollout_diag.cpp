@@ -5,25 +5,27 @@
 #include <vector>
 #include <algorithm>
 
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
 int main(int argc, char** argv) {
     long long n = argc > 1 ? atoll(argv[1]) : (1 << 20);
     int reps = argc > 2 ? atoi(argv[2]) : 5;
     uint64_t *fb; int8_t* df; uint8_t* pl; int64_t* hist; unsigned long long* diag;
-    hipMalloc(&fb, n * 16); hipMalloc(&df, n); hipMalloc(&pl, n); hipMalloc(&hist, 133 * 8);
+    CK(hipMalloc(&fb, n * 16)); CK(hipMalloc(&df, n)); CK(hipMalloc(&pl, n)); CK(hipMalloc(&hist, 133 * 8));
     const long long maxw = 1 << 20;
-    hipMalloc(&diag, maxw * 32);
-    hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag));
-    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    CK(hipMalloc(&diag, maxw * 32));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag)));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int r = 0; r < reps; r++) {
-        hipMemset(hist, 0, 133 * 8);
-        hipMemset(diag, 0, maxw * 32);
-        hipEventRecord(e0, 0);
+        CK(hipMemset(hist, 0, 133 * 8));
+        CK(hipMemset(diag, 0, maxw * 32));
+        CK(hipEventRecord(e0, 0));
         int st = oth_rollout(nullptr, nullptr, 0x5EED, (uint64_t)r * n, 0, 10, fb, df, pl, nullptr, hist, n, nullptr);
-        hipEventRecord(e1, 0);
-        hipDeviceSynchronize();
-        float ms; hipEventElapsedTime(&ms, e0, e1);
-        std::vector<long long> h(133); hipMemcpy(h.data(), hist, 133 * 8, hipMemcpyDeviceToHost);
-        std::vector<unsigned long long> d(maxw * 4); hipMemcpy(d.data(), diag, maxw * 32, hipMemcpyDeviceToHost);
+        CK(hipEventRecord(e1, 0));
+        CK(hipDeviceSynchronize());
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        std::vector<long long> h(133); CK(hipMemcpy(h.data(), hist, 133 * 8, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> d(maxw * 4); CK(hipMemcpy(d.data(), diag, maxw * 32, hipMemcpyDeviceToHost));
         long long waves = 0; unsigned long long t0 = ~0ull, t1 = 0; double life = 0; double it = 0; unsigned long long maxit = 0, minit = ~0ull;
         std::vector<double> lifes;
         for (long long w = 0; w < maxw; w++) { if (!d[4*w+1]) continue; waves++; t0 = std::min(t0, d[4*w]); t1 = std::max(t1, d[4*w+1]); }

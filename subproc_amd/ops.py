@@ -22,8 +22,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BLACK, BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, PASS, POLICY_EVAL, POLICY_GREEDY,
-                   POLICY_RANDOM, POS_STRIDE, WHITE, check)
+from ._lib import (BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, POLICY_EVAL, POLICY_GREEDY, POLICY_RANDOM,
+                   POS_STRIDE, check)
 from .params import DEFAULT_WEIGHTS, as_weights
 
 StepResult = namedtuple("StepResult", "boards turn flips legal_next ret")

@@ -5,7 +5,6 @@ Called through the product's own ctypes signature table with host buffers and
 checked against the golden fixtures from the real board.py; the GPU twin of
 these calls is tests/test_gpu_abi_pair.py.  CPU only."""
 import ctypes
-import os
 import re
 import subprocess
 

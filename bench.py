@@ -13,6 +13,7 @@ histogram, passes included) of ALL ranks / max-over-ranks wall time.
 Also reported on rank 0 (secondary, same JSON line):
   * step_65536 : config 2, one oth_step launch over 65,536 reachable mid-game
     positions (52 algorithmic HBM bytes per step), repeated launches;
+  * step_65536_graph: the same 65,536-board launches captured in a HIP graph;
   * step_steady: the same kernel over 16,777,216 positions (HBM roofline);
   * rollout_16M: the config-3 kernel on 16,777,216 games per launch (the
     per-launch tail amortised: the kernel's steady-state rate);
@@ -222,6 +223,7 @@ def main():
         if args.workload != "step":
             guarded("step_65536", lambda: _bench_step(ops, torch, dev, stream, args, 65536, 1, torch.cuda.synchronize,
                                                       lambda x: x, launches=200))
+            guarded("step_65536_graph", lambda: _bench_step_graph(ops, torch, dev, args))
             guarded("step_steady_16M", lambda: _bench_step(ops, torch, dev, stream, args, 1 << 24, 1,
                                                            torch.cuda.synchronize, lambda x: x, launches=10))
         # BENCH_SKIP (comma list) drops secondary lines; tools/profile_round.sh skips
@@ -285,6 +287,35 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
         r["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s", "frac": va / VALU_PEAK_WINSTR,
                      "busy_pmc": prof.get("valu_busy")}
     return r
+
+
+def _bench_step_graph(ops, torch, dev, args, n=65536, launches=200):
+    """config 2 with the launch-bound loop captured in a HIP graph (one replay =
+    `launches` oth_step launches; the C-ABI launches on the capturing stream)."""
+    from subproc_amd import _lib
+
+    lib = _lib.load()
+    pos = ops.sample_midgame(n, args.seed, index0=0, device=dev)
+    bo, to = torch.empty_like(pos.boards), torch.empty_like(pos.turn)
+    fl, ln = torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev)
+    rt = torch.empty(n, dtype=torch.int8, device=dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream().cuda_stream
+        for _ in range(launches):
+            _lib.check(lib.oth_step(pos.boards.data_ptr(), pos.turn.data_ptr(), pos.move.data_ptr(), bo.data_ptr(),
+                                    to.data_ptr(), fl.data_ptr(), ln.data_ptr(), rt.data_ptr(), None, n, st),
+                       "oth_step")
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "env-steps/sec (batched step, HIP graph of %d launches)" % launches,
+            "value": n * launches / dt, "unit": "env-steps/s", "batch": n, "launches": launches,
+            "us_per_launch": dt / launches * 1e6}
 
 
 def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):

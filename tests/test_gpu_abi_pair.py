@@ -139,3 +139,40 @@ def test_td_pair():
     out = Buf(np.zeros(len(uk), np.float64))
     both("oth_td_ema", sv, seg, init, 0.03, 1 - 0.03, out, len(uk))
     same(out)
+
+
+def test_empty_null_and_invalid_arguments():
+    """n = 0 is a no-op for every entry point; optional outputs may be NULL;
+    bad arguments return OTH_EINVAL before anything is launched (both builds)."""
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    st = torch.cuda.current_stream().cuda_stream
+    w = (ctypes.c_int8 * 36)()
+    for lib, s in ((gpu, st), (cpu, None)):
+        assert lib.oth_reset(None, None, None, 0, s) == 0
+        assert lib.oth_legal(None, None, None, 0, s) == 0
+        assert lib.oth_step(None, None, None, None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_result(None, None, None, None, None, 0, s) == 0
+        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_rollout_eval(None, None, 1, 0, 0, w, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, w, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_replay(None, None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_book_text(None, None, 0, None, s) == 0
+        assert lib.oth_features(None, None, None, 0, s) == 0
+        assert lib.oth_eval(None, None, w, None, 0, s) == 0
+        assert lib.oth_td_updates(None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 0, s) == 0
+        assert lib.oth_sample_midgame(1, 0, None, None, None, None, 0, s) == 0
+        E = _lib.OTH_EINVAL
+        assert lib.oth_step(None, None, None, None, None, None, None, None, None, 5, s) == E
+        assert lib.oth_rollout(None, None, 1, 0, 3, 0, None, None, None, None, None, 5, s) == E  # bad policy
+        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, -1, s) == E
+        assert lib.oth_rollout_eval(None, None, 1, 0, 0, None, None, None, None, None, None, 5, s) == E
+        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, None, None, None, None, None, None, 5, s) == E
+        assert lib.oth_eval(None, None, None, None, 0, s) == E
+        assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 3, s) == E
+    # every rollout output may be NULL: only the histogram is produced
+    n = 4096
+    hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))
+    both("oth_rollout", None, None, 12, 0, 0, 10, None, None, None, None, hist, n)
+    same(hist)
+    assert int(hist.h[:129].sum()) == n

@@ -63,7 +63,7 @@ class VecEnv:
         return ops.result(self.boards).terminal.bool()
 
     def books(self):
-        """Book text (serialize_str, board.py:214-221) of every game, host side."""
-        b = ops.to_numpy_u64(self.boards)
-        t = self.turn.cpu().tolist()
-        return [s + " " + codec.string_from_turn(tt) for s, tt in zip(codec.serialize_boards(b), t)]
+        """Book text (serialize_str, board.py:214-221) of every game: oth_book_text
+        on the device, one 67-byte line per game, decoded on the host."""
+        raw = ops.book_text(self.boards, self.turn).cpu().numpy().tobytes()
+        return raw.decode("ascii").splitlines()

@@ -95,6 +95,11 @@ def test_vecenv_random_games_match_fixture():
     np.testing.assert_array_equal(res["diff"].cpu().numpy(), z["diff"])
     books = env.books()
     assert all(len(s) == 66 for s in books)
+    # the device text equals the host codec (pinned to board.py by tests/test_codec.py)
+    from subproc_amd import codec
+    host = [b + " " + codec.string_from_turn(t)
+            for b, t in zip(codec.serialize_boards(ops.to_numpy_u64(env.boards)), env.turn.cpu().tolist())]
+    assert books == host
 
 
 def test_vecenv_strings():

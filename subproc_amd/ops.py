@@ -50,11 +50,13 @@ def ctypes_stream(s):
     return s.cuda_stream  # hipStream_t as an integer handle
 
 
-def _dev(t, name, dtype, shape=None):
+def _dev(t, name, dtype, shape=None, device=None):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name}: expected a torch.Tensor")
     if t.device.type != "cuda":
         raise ValueError(f"{name}: tensor must be on a ROCm device (got {t.device}); there is no CPU path")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: tensor is on {t.device}, expected {device} (all arguments on one device)")
     if t.dtype != dtype:
         raise TypeError(f"{name}: expected dtype {dtype}, got {t.dtype}")
     if not t.is_contiguous():
@@ -64,8 +66,8 @@ def _dev(t, name, dtype, shape=None):
     return t.data_ptr()
 
 
-def _opt(t, name, dtype, shape):
-    return None if t is None else _dev(t, name, dtype, shape)
+def _opt(t, name, dtype, shape, device=None):
+    return None if t is None else _dev(t, name, dtype, shape, device)
 
 
 def _n(boards):
@@ -78,6 +80,8 @@ def _device(device):
     d = torch.device(device)
     if d.type != "cuda":
         raise ValueError(f"device must be a ROCm device, got {d}")
+    if d.index is None:  # "cuda" -> the current device, so it compares equal to tensors' devices
+        d = torch.device("cuda", torch.cuda.current_device())
     return d
 
 
@@ -97,10 +101,10 @@ def legal(boards, turn, out=None):
     """Legal-move bitboard of the side to move (Board.puttables as a mask)."""
     n = _n(boards)
     pb = _dev(boards, "boards", torch.int64)
-    pt = _dev(turn, "turn", torch.uint8, (n,))
+    pt = _dev(turn, "turn", torch.uint8, (n,), boards.device)
     if out is None:
         out = torch.empty(n, dtype=torch.int64, device=boards.device)
-    po = _dev(out, "out", torch.int64, (n,))
+    po = _dev(out, "out", torch.int64, (n,), boards.device)
     with torch.cuda.device(boards.device):
         check(_lib.load().oth_legal(pb, pt, po, n, _stream()), "oth_legal")
     return out
@@ -116,9 +120,9 @@ def step(boards, turn, move, nturn=None, inplace=False, want_flips=True, want_le
     """
     n = _n(boards)
     pb = _dev(boards, "boards", torch.int64)
-    pt = _dev(turn, "turn", torch.uint8, (n,))
-    pm = _dev(move, "move", torch.uint8, (n,))
-    pn = _opt(nturn, "nturn", torch.uint8, (n,))
+    pt = _dev(turn, "turn", torch.uint8, (n,), boards.device)
+    pm = _dev(move, "move", torch.uint8, (n,), boards.device)
+    pn = _opt(nturn, "nturn", torch.uint8, (n,), boards.device)
     dev = boards.device
     bo = boards if inplace else torch.empty_like(boards)
     to = turn if inplace else torch.empty_like(turn)
@@ -172,14 +176,14 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
         if _n(start) != n:
             raise ValueError("start must have n rows")
         ps = _dev(start, "start", torch.int64)
-        pst = _opt(start_turn, "start_turn", torch.uint8, (n,))
+        pst = _opt(start_turn, "start_turn", torch.uint8, (n,), start.device)
     fb = torch.empty((n, 2), dtype=torch.int64, device=d) if want_boards else None
     df = torch.empty(n, dtype=torch.int8, device=d) if want_diff else None
     pl = torch.empty(n, dtype=torch.uint8, device=d) if want_plies else None
     mv = torch.empty((n, MOVES_STRIDE), dtype=torch.uint8, device=d) if record_moves else None
     if hist is None:
         hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=d)
-    ph = _dev(hist, "hist", torch.int64, (HIST_BINS,))
+    ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
 
     def ptr(t):
         return None if t is None else t.data_ptr()
@@ -221,9 +225,9 @@ def replay(moves, plies, start=None, start_turn=None):
     is_game_over(); game i's positions are rows 0..plies[i]."""
     n = moves.shape[0]
     pm = _dev(moves, "moves", torch.uint8, (n, MOVES_STRIDE))
-    pp = _dev(plies, "plies", torch.uint8, (n,))
-    ps = _opt(start, "start", torch.int64, (n, 2))
-    pst = _opt(start_turn, "start_turn", torch.uint8, (n,))
+    pp = _dev(plies, "plies", torch.uint8, (n,), moves.device)
+    ps = _opt(start, "start", torch.int64, (n, 2), moves.device)
+    pst = _opt(start_turn, "start_turn", torch.uint8, (n,), moves.device)
     dev = moves.device
     b = torch.zeros((n, POS_STRIDE, 2), dtype=torch.int64, device=dev)
     t = torch.zeros((n, POS_STRIDE), dtype=torch.uint8, device=dev)
@@ -239,7 +243,7 @@ def book_text(boards, turn):
     a uint8 tensor of n * 67 bytes on the device."""
     n = _n(boards)
     pb = _dev(boards, "boards", torch.int64)
-    pt = _dev(turn, "turn", torch.uint8, (n,))
+    pt = _dev(turn, "turn", torch.uint8, (n,), boards.device)
     out = torch.empty(n * BOOK_LINE, dtype=torch.uint8, device=boards.device)
     with torch.cuda.device(boards.device):
         check(_lib.load().oth_book_text(pb, pt, n, out.data_ptr(), _stream()), "oth_book_text")
@@ -252,7 +256,7 @@ def features(boards, side):
     (64 - n_empty, n_puttable_for(side), 8 region mask_counts)."""
     n = _n(boards)
     pb = _dev(boards, "boards", torch.int64)
-    ps = _dev(side, "side", torch.uint8, (n,))
+    ps = _dev(side, "side", torch.uint8, (n,), boards.device)
     out = torch.empty((n, N_FEATURES), dtype=torch.uint8, device=boards.device)
     with torch.cuda.device(boards.device):
         check(_lib.load().oth_features(pb, ps, out.data_ptr(), n, _stream()), "oth_features")
@@ -265,7 +269,7 @@ def evaluate(boards, side, weights=None):
     the model progress_position_moves_learn.py:160-184 fits)."""
     n = _n(boards)
     pb = _dev(boards, "boards", torch.int64)
-    ps = _dev(side, "side", torch.uint8, (n,))
+    ps = _dev(side, "side", torch.uint8, (n,), boards.device)
     out = torch.empty(n, dtype=torch.int32, device=boards.device)
     with torch.cuda.device(boards.device):
         check(_lib.load().oth_eval(pb, ps, _weights_ptr(weights), out.data_ptr(), n, _stream()), "oth_eval")

@@ -374,3 +374,13 @@ def test_concurrent_rollouts_on_two_streams():
     torch.cuda.synchronize()
     for a, b in zip(seq, outs):
         assert torch.equal(a.final_boards, b.final_boards) and torch.equal(a.hist, b.hist)
+
+
+def test_mixed_device_and_cpu_arguments_are_rejected():
+    b, t, nt = ops.reset(8, "cuda")
+    with pytest.raises(ValueError):
+        ops.step(b, t.cpu(), torch.zeros(8, dtype=torch.uint8, device=DEV))
+    with pytest.raises(ValueError):
+        ops.rollout(8, 1, hist=torch.zeros(133, dtype=torch.int64), device=DEV)
+    r = ops.rollout(8, 1, hist=torch.zeros(133, dtype=torch.int64, device=DEV), device="cuda")  # "cuda" == cuda:0
+    assert int(r.hist[:129].sum()) == 8

@@ -19,23 +19,45 @@ policy into GameRunner unchanged:
 
 Rules and move generation run on the GPU through the drop-in Board
 (subproc_amd.board); the move choice is the env's policy: "random" (uniform
-over legal moves, seeded) or "greedy" (minimise the opponent's mobility, ties
-to the first move in puttables order).
+over legal moves, seeded), "greedy" (minimise the opponent's mobility, ties
+to the first move in puttables order) or "eval" (maximise the mover's linear
+eval of the child under an eval table, ties likewise -- the kernels' eval
+policy).  ``--params FILE`` loads the table from the file paramgen.py writes
+(paramgen.py:12-19), the file the reference's own engines read.
 """
 import argparse
 import random
 import sys
 
+import numpy as np
+import torch
+
 from . import board as gboard
+from . import ops, params
 from .codec import handstr_from_coord
 
 
 class Engine:
-    def __init__(self, name="GPU", policy="greedy", seed=0):
+    def __init__(self, name="GPU", policy="greedy", seed=0, weights=None):
         self.name = name
         self.policy = policy
         self.rng = random.Random(seed)
+        self.weights = params.as_weights(params.DEFAULT_WEIGHTS if weights is None else weights)
         self.board = gboard.Board()
+
+    def _choose_eval(self, puts):
+        """All children in one oth_step launch, their evals in one oth_eval launch."""
+        b = self.board
+        bl, wh = b.bitboards()
+        n = len(puts)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        boards = ops.from_numpy_u64(np.array([[bl, wh]] * n, np.uint64), dev)
+        side = torch.full((n,), b.turn, dtype=torch.uint8, device=dev)
+        sq = torch.tensor([x + 8 * y for (x, y) in puts], dtype=torch.uint8, device=dev)
+        children = ops.step(boards, side, sq, want_flips=False, want_legal=False).boards
+        ev = ops.evaluate(children, side, self.weights).cpu().tolist()
+        k = max(range(n), key=lambda i: (ev[i], -i))  # puts is LSB-first: ties -> lowest square
+        return handstr_from_coord(*puts[k])
 
     def choose(self):
         b = self.board
@@ -45,6 +67,8 @@ class Engine:
         if self.policy == "random":
             x, y = puts[self.rng.randrange(len(puts))]
             return handstr_from_coord(x, y)
+        if self.policy == "eval":
+            return self._choose_eval(puts)
         best, bestv = None, None
         opp = b.hostile(b.turn)
         for (x, y) in puts:
@@ -70,7 +94,8 @@ class Engine:
             out(">%s plays %s%s" % (self.name, color, mv.upper() if mv != "PS" else "PS"))
             out("")
         elif cmd == "verbose p":
-            out("%s policy=%s" % (self.name, self.policy))
+            extra = " weights=%s" % self.weights.reshape(-1).tolist() if self.policy == "eval" else ""
+            out("%s policy=%s%s" % (self.name, self.policy, extra))
         elif cmd == "verbose 1":
             text = str(self.board).rstrip("\n").split("\n")
             text += [""] * (13 - len(text))
@@ -93,10 +118,12 @@ class Engine:
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     p.add_argument("--name", default="GPU")
-    p.add_argument("--policy", choices=["random", "greedy"], default="greedy")
+    p.add_argument("--policy", choices=["random", "greedy", "eval"], default="greedy")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--params", default=None, help="eval table in the paramgen.py file format (policy eval)")
     a = p.parse_args(argv)
-    eng = Engine(a.name, a.policy, a.seed)
+    weights = params.read_paramgen(a.params)[1] if a.params else None
+    eng = Engine(a.name, a.policy, a.seed, weights)
 
     def out(s):
         sys.stdout.write(s + "\n")

@@ -91,3 +91,39 @@ def test_engine_plays_full_game(pa, pb):
         bl, wh = o["boards"][0, k]
         assert oracle.serialize_str(bl, wh, o["turn"][0, k]) == line
     assert o["end"][0, len(moves)] == 1
+
+
+def test_engine_eval_choice_equals_kernel_policy(tmp_path):
+    """--policy eval picks exactly what the kernels' eval policy picks (first
+    move of an eval rollout with n_random = 0 from the same position), with the
+    table read from a paramgen-format file."""
+    from subproc_amd import engine, ops, params
+    w = np.random.default_rng(21).integers(-127, 128, (4, 9)).astype(np.int8)
+    path = tmp_path / "param.bin"
+    params.write_paramgen(path, w)
+    eng = engine.Engine(policy="eval", weights=params.read_paramgen(path)[1])
+    pos = ops.sample_midgame(48, 77, device="cuda")
+    r = ops.rollout(48, 5, 0, "eval", 0, start=pos.boards, start_turn=pos.turn, record_moves=True, weights=w,
+                    device="cuda")
+    first = r.moves[:, 0].cpu().tolist()
+    bits = ops.to_numpy_u64(pos.boards)
+    for i in range(48):
+        eng.board = gboard.Board()
+        eng.board._set_bits(int(bits[i, 0]), int(bits[i, 1]))
+        eng.board.turn = int(pos.turn[i])
+        assert codec.move_code(eng.choose().lower()) == first[i], i
+
+
+def test_engine_eval_process_with_paramgen_file(tmp_path):
+    from subproc_amd import params
+    path = tmp_path / "param.bin"
+    params.write_paramgen(path, params.DEFAULT_WEIGHTS)
+    black = Player(["--policy", "eval", "--params", str(path), "--name", "GPU-eval"])
+    white = Player(["--policy", "random", "--name", "GPU-random", "--seed", "3"])
+    try:
+        final, moves, record = play_a_game(black, white)
+    finally:
+        for p in (black, white):
+            if p.proc.poll() is None:
+                p.proc.kill()
+    assert final.is_game_over() and black.name == "GPU-eval"

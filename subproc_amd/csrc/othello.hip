@@ -234,17 +234,10 @@ __global__ __launch_bounds__(kBlock) void legal_kernel(const u64* __restrict__ b
     legal[i] = m;
 }
 
-__global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in,
-                                                      const uint8_t* turn_in,
-                                                      const uint8_t* __restrict__ move, u64* boards_out,
-                                                      uint8_t* turn_out, u64* __restrict__ flips_out,
-                                                      u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
-                                                      uint8_t* __restrict__ nturn, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
-    const u32 t = turn_in[i];
-    const u32 mvc = move[i];
+// one board of the step (board.py:192-209 semantics, see include/othello.h)
+__device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 mvc, u64* boards_out, uint8_t* turn_out,
+                                           u64* __restrict__ flips_out, u64* __restrict__ legal_next,
+                                           int8_t* __restrict__ ret_out, uint8_t* __restrict__ nturn) {
     const bool valid_turn = (t == OTH_BLACK) | (t == OTH_WHITE);
     const bool black = t == OTH_BLACK;
     u64 P = black ? b.x : b.y;
@@ -282,6 +275,17 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in,
     if (flips_out) flips_out[i] = f;
     if (ret_out) ret_out[i] = (int8_t)r;
     if (nturn && moved) nturn[i] = (uint8_t)(nturn[i] + 1);
+}
+
+__global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, const uint8_t* turn_in,
+                                                      const uint8_t* __restrict__ move, u64* boards_out,
+                                                      uint8_t* turn_out, u64* __restrict__ flips_out,
+                                                      u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
+                                                      uint8_t* __restrict__ nturn, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    step_board(i, reinterpret_cast<const ulonglong2*>(boards_in)[i], turn_in[i], move[i], boards_out, turn_out,
+               flips_out, legal_next, ret_out, nturn);
 }
 
 __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ boards, uint8_t* __restrict__ nb,

@@ -325,7 +325,8 @@ struct RolloutArgs {
     uint8_t* moves;
     long long* hist;
     int64_t n;
-    unsigned long long* work;  // batch counter, zeroed before the launch
+    unsigned long long* work;  // batch counter slot (monotonic across launches)
+    u64 work_base;             // its value when this launch starts (host-tracked)
     EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table
 };
 
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     for (;;) {
         // ---- dequeue a batch of 64 games (one per lane)
         u64 base = 0;
-        if (lane == 0) base = atomicAdd(a.work, 64ull);
+        if (lane == 0) base = atomicAdd(a.work, 64ull) - a.work_base;
         base = __shfl(base, 0);
         if (base >= n) break;  // wave-uniform
 
@@ -871,11 +872,18 @@ struct DeviceState {
     std::atomic<int> ready{0};
     Tuning tuning;
     unsigned long long* work = nullptr;
+    // Host shadow of each counter slot.  A launch of B batches on W waves
+    // advances its slot by exactly 64 * (B + W) (every batch is one successful
+    // dequeue, every wave ends on one failing dequeue), so the next launch on
+    // the slot knows its starting value without a reset on the stream.  A slot
+    // whose launch failed is reset with a memset before its next use.
+    std::atomic<unsigned long long> slot_base[kWorkSlots];
+    std::atomic<bool> slot_dirty[kWorkSlots];
 };
 DeviceState g_dev[kMaxDevices];
 std::mutex g_dev_mu;
 
-const DeviceState* device_state() {
+DeviceState* device_state() {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= kMaxDevices) return nullptr;
@@ -969,15 +977,24 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
         a.ew[0].w[k] = w_black ? w_black[k] : 0;
         a.ew[1].w[k] = w_white ? w_white[k] : 0;
     }
-    const DeviceState* ds = device_state();
+    DeviceState* ds = device_state();
     if (!ds) return status(hipErrorInvalidDevice);
     const Tuning& t = ds->tuning;
     const int slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
     a.work = ds->work + (size_t)slot * kCtrStride;
-    hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
-    if (e != hipSuccess) return status(e);
+    DeviceState& dsm = *ds;
+    if (dsm.slot_dirty[slot].exchange(false)) {
+        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
+        if (e != hipSuccess) {
+            dsm.slot_dirty[slot].store(true);
+            return status(e);
+        }
+        dsm.slot_base[slot].store(0);
+    }
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
+    const u64 advance = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64));
+    a.work_base = dsm.slot_base[slot].fetch_add(advance);
     hipStream_t st = (hipStream_t)stream;
     if (policy == OTH_POLICY_EVAL) {
         if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
@@ -989,7 +1006,9 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
         if (moves) rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
-    return launched();
+    const int rc = launched();
+    if (rc != OTH_OK) dsm.slot_dirty[slot].store(true);  // counter state unknown: reset before reuse
+    return rc;
 }
 }  // namespace
 

@@ -384,3 +384,15 @@ def test_mixed_device_and_cpu_arguments_are_rejected():
         ops.rollout(8, 1, hist=torch.zeros(133, dtype=torch.int64), device=DEV)
     r = ops.rollout(8, 1, hist=torch.zeros(133, dtype=torch.int64, device=DEV), device="cuda")  # "cuda" == cuda:0
     assert int(r.hist[:129].sum()) == 8
+
+
+def test_counter_slots_survive_reuse():
+    """oth_rollout keeps no reset on the stream: each of the 64 work-counter slots
+    advances by a host-tracked 64 * (batches + waves) per launch.  130 launches
+    (every slot reused twice, sizes varying) must all equal their reference."""
+    ref = {n: ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False).hist
+           for n in (1, 64, 1000, 5000)}
+    for k in range(130):
+        n = (1, 64, 1000, 5000)[k % 4]
+        r = ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False)
+        assert torch.equal(r.hist, ref[n]), (k, n)

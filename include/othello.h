@@ -20,7 +20,9 @@
  *   - every pointer is DEVICE memory owned by the caller (e.g. torch tensors);
  *     the library allocates nothing persistent;
  *   - calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
- *     and thread-safe on distinct streams;
+ *     and thread-safe on distinct streams; they may be captured in a hipGraph
+ *     (a captured rollout resets its own work counter on every replay); up to
+ *     64 rollouts (and 64 captured ones) may execute concurrently;
  *   - return value: OTH_OK (0), OTH_EINVAL (invalid argument, nothing launched),
  *     or -(hipError_t) of the failed launch.  Per-game semantics (illegal
  *     move ...) are reported in `ret`, never as a status.

@@ -310,8 +310,11 @@ __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ 
 // per-lane refill, DESIGN.md §Rollout scheduling).
 // ---------------------------------------------------------------------------
 constexpr int kWorkSlots = 64;  // concurrent launches supported (distinct streams)
+// captured launches (hipGraph) use their own slots: a replay cannot update the
+// host shadow, so a captured launch records a memset node and starts from 0
+constexpr int kGraphSlots = 64;
 constexpr int kCtrStride = 16;  // u64 words between counters (128 B)
-__device__ unsigned long long g_work[kWorkSlots * kCtrStride];
+__device__ unsigned long long g_work[(kWorkSlots + kGraphSlots) * kCtrStride];
 
 struct RolloutArgs {
     const u64* start;
@@ -859,6 +862,7 @@ struct Tuning {
     unsigned resident_blocks[3];  // per policy
 };
 std::atomic<unsigned long long> g_slot{0};
+std::atomic<unsigned long long> g_graph_slot{0};
 
 int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
@@ -980,21 +984,33 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     DeviceState* ds = device_state();
     if (!ds) return status(hipErrorInvalidDevice);
     const Tuning& t = ds->tuning;
-    const int slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
-    a.work = ds->work + (size_t)slot * kCtrStride;
-    DeviceState& dsm = *ds;
-    if (dsm.slot_dirty[slot].exchange(false)) {
-        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
-        if (e != hipSuccess) {
-            dsm.slot_dirty[slot].store(true);
-            return status(e);
-        }
-        dsm.slot_base[slot].store(0);
-    }
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
-    const u64 advance = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64));
-    a.work_base = dsm.slot_base[slot].fetch_add(advance);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
+    DeviceState& dsm = *ds;
+    int slot = -1;
+    if (cap == hipStreamCaptureStatusActive) {
+        // a graph node: every replay resets its own slot first
+        const int gs = (int)(g_graph_slot.fetch_add(1, std::memory_order_relaxed) % kGraphSlots);
+        a.work = ds->work + (size_t)(kWorkSlots + gs) * kCtrStride;
+        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
+        if (e != hipSuccess) return status(e);
+        a.work_base = 0;
+    } else {
+        slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
+        a.work = ds->work + (size_t)slot * kCtrStride;
+        if (dsm.slot_dirty[slot].exchange(false)) {
+            hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
+            if (e != hipSuccess) {
+                dsm.slot_dirty[slot].store(true);
+                return status(e);
+            }
+            dsm.slot_base[slot].store(0);
+        }
+        const u64 advance = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64));
+        a.work_base = dsm.slot_base[slot].fetch_add(advance);
+    }
     hipStream_t st = (hipStream_t)stream;
     if (policy == OTH_POLICY_EVAL) {
         if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
@@ -1007,7 +1023,7 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
     const int rc = launched();
-    if (rc != OTH_OK) dsm.slot_dirty[slot].store(true);  // counter state unknown: reset before reuse
+    if (rc != OTH_OK && slot >= 0) dsm.slot_dirty[slot].store(true);  // counter state unknown: reset before reuse
     return rc;
 }
 }  // namespace

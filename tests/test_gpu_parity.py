@@ -396,3 +396,29 @@ def test_counter_slots_survive_reuse():
         n = (1, 64, 1000, 5000)[k % 4]
         r = ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False)
         assert torch.equal(r.hist, ref[n]), (k, n)
+
+
+def test_rollout_captured_in_a_graph_replays_correctly():
+    """A captured oth_rollout records its own counter reset (graph slots), so
+    every replay plays all games; eager launches on the normal slots before and
+    after the replays are unaffected."""
+    n = 3000
+    ref = ops.rollout(n, 9, 50, device=DEV)
+    fb = torch.empty((n, 2), dtype=torch.int64, device=DEV)
+    hist = torch.zeros(133, dtype=torch.int64, device=DEV)
+    from subproc_amd import _lib
+    lib = _lib.load()
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(lib.oth_rollout(None, None, 9, 50, 0, 10, fb.data_ptr(), None, None, None, hist.data_ptr(), n, st),
+                   "oth_rollout")
+    for k in range(3):
+        hist.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(fb, ref.final_boards), k
+        assert torch.equal(hist, ref.hist), k
+        mid = ops.rollout(n, 9, 50, device=DEV)
+        assert torch.equal(mid.hist, ref.hist), k

@@ -37,11 +37,35 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md
-# VALU issue ceiling for this code's instruction mix: every VALU instruction of
-# these kernels occupies its SIMD for one quad-cycle (measured: SQ_ACTIVE_INST_VALU
-# == SQ_INSTS_VALU; tools/diag/valu_rate*.cpp), 1024 SIMDs at the 2.4 GHz max clock
-VALU_PEAK_WINSTR = 1024 * 2.4e9 / 4
+# VALU issue: a wave64 instruction can issue every 2 cycles on a SIMD-32
+# (MI355X_MICROARCH.md), 1024 SIMDs at the 2.4 GHz max clock.  Measured on the
+# box (tools/diag/valu_rate*.cpp) only plain VOP2 logic reaches that (~2.2
+# cycles); the 64-bit shifts, bfi, bcnt, cndmask ... these kernels are made of
+# take ~4.  The ceiling priced for a kernel is therefore its hot loop's
+# mix-weighted mean (tools/valu_mix.py -> profiles/valu_mix.json).
+VALU_PEAK_HW = 1024 * 2.4e9 / 2
+
+
+def valu_entry(kernel, achieved, **extra):
+    """VALU roofline of `kernel` at `achieved` wave-instructions/s."""
+    peak, mix = VALU_PEAK_HW, None
+    try:
+        with open(os.path.join(ROOT, "profiles", "valu_mix.json")) as f:
+            mix = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        pass
+    if mix:
+        peak = mix["peak_winstr_s"]
+    e = {"achieved": achieved, "peak": peak, "unit": "wave-instr/s", "frac": achieved / peak,
+         "peak_basis": ("hot-loop mix, %.2f cycles/instr (profiles/valu_mix.json)" % mix["mean_cycles"]) if mix
+         else "2 cycles/instr (SIMD-32 issue)",
+         "frac_of_2cycle_issue": achieved / VALU_PEAK_HW}
+    e.update(extra)
+    return e
+
+
 STEP_BYTES = 52  # algorithmic bytes per oth_step (SURVEY.md §8d): in 16+1+1, out 16+1+8+8+1
+LAUNCH_EVENTS = os.environ.get("BENCH_LAUNCH_EVENTS", "1") == "1"
 ROLLOUT_BYTES_PER_GAME = 18  # final board 16 + diff 1 + plies 1 written; opening generated in-kernel
 
 
@@ -68,8 +92,10 @@ def profile_entry(kernels, name, grid=None):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--prewarm-ms", type=float, default=300.0,
+                   help="untimed rollout launches before the warmup steps, so the GPU clock has ramped")
     p.add_argument("--workload", choices=["rollout", "greedy", "step"], default="rollout")
     p.add_argument("--games", type=int, default=1 << 20, help="games per GPU per bench step (rollout workloads)")
     p.add_argument("--seed", type=int, default=0x5EED)
@@ -79,6 +105,8 @@ def parse():
     p.add_argument("--allreduce", choices=["async", "sync", "end"], default="end",
                    help="histogram all-reduce at N>1: per step overlapped with the next step (async), "
                         "per step blocking (sync), or once over all timed steps (end)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="HIP streams the rollout steps are issued on round-robin (1 = serialized)")
     return p.parse_args()
 
 
@@ -101,7 +129,6 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from subproc_amd import ops
-    from subproc_amd._lib import HIST_BINS
 
     stream = torch.cuda.current_stream()
 
@@ -117,96 +144,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    n = args.games
     policy = "greedy" if args.workload == "greedy" else "random"
     out = {}
 
     if args.workload in ("rollout", "greedy"):
-        hists = torch.zeros((args.warmup + args.steps, HIST_BINS), dtype=torch.int64, device=dev)
-        fb = torch.empty((n, 2), dtype=torch.int64, device=dev)
-        df = torch.empty(n, dtype=torch.int8, device=dev)
-        pl = torch.empty(n, dtype=torch.uint8, device=dev)
-        from subproc_amd import _lib
-
-        lib = _lib.load()
-        pid = 0 if policy == "random" else 1
-
-        pending = []
-
-        def one_step(s):
-            # bench step s plays global game ids [(s*world + rank)*n, +n): fresh games every step
-            h = hists[s]
-            _lib.check(lib.oth_rollout(None, None, args.seed, (s * world + rank) * n, pid, 10, fb.data_ptr(),
-                                       df.data_ptr(), pl.data_ptr(), None, h.data_ptr(), n, stream.cuda_stream),
-                       "oth_rollout")
-            if use_dist and args.allreduce != "end":
-                # config 4: the one collective.  Async on RCCL's stream, so it overlaps the
-                # next step's rollout (each step owns its histogram row); all are waited
-                # for inside the timed region.
-                work = dist.all_reduce(h, op=dist.ReduceOp.SUM, async_op=args.allreduce == "async")
-                if work is not None:
-                    pending.append(work)
-
-        def drain():
-            while pending:
-                pending.pop().wait()
-
-        for s in range(args.warmup):
-            one_step(s)
-        drain()
-        barrier()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for k, s in enumerate(range(args.warmup, args.warmup + args.steps)):
-            one_step(s)
-            step_ev[k].record(stream)
-        if use_dist and args.allreduce == "end":
-            total = hists[args.warmup:].sum(0)
-            dist.all_reduce(total, op=dist.ReduceOp.SUM)
-            hists[args.warmup].copy_(total)
-            hists[args.warmup + 1:].zero_()
-        ev1.record(stream)
-        drain()
-        barrier()
-        t1 = time.perf_counter()
-        elapsed = max_over_ranks(t1 - t0)
-        kern_ms = ev0.elapsed_time(ev1) / args.steps  # stream-ordered: the rollout launch (+ all-reduce at N>1)
-        # per-step stream time (launch + counter memset), median over the K timed steps
-        per_step = sorted([ev0.elapsed_time(step_ev[0])] +
-                          [step_ev[k - 1].elapsed_time(step_ev[k]) for k in range(1, args.steps)])
-        median_ms = per_step[len(per_step) // 2] if len(per_step) % 2 else \
-            0.5 * (per_step[len(per_step) // 2 - 1] + per_step[len(per_step) // 2])
-        timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) when distributed
-        env_steps = int(timed[132])
-        games = n * world * args.steps
-        value = env_steps / elapsed
-        out.update(metric="env-steps/sec (batched self-play)", value=value, unit="env-steps/s",
-                   n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
-                   higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u64",
-                   data="synthetic (games from the opening, counter-based RNG seed %#x)" % args.seed,
-                   config={"workload": "config%d: %s-policy self-play rollouts to terminal" %
-                           (3 if policy == "random" and world == 1 else 4 if policy == "random" else 5, policy),
-                           "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
-                           "env_steps_per_game": env_steps / games})
-        per_launch_games = n
-        achieved = per_launch_games * ROLLOUT_BYTES_PER_GAME / (kern_ms * 1e-3) / 1e9
-        kname = "rollout_kernel<%d, false>" % pid
-        pfile, kernels = load_profile()
-        prof = profile_entry(kernels, kname) if n == 1 << 20 else None
-        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS,
-                           "traffic": prof.get("hbm_bytes") if prof else None,
-                           "kernel": kname, "launch_ms": kern_ms, "launch_ms_median": median_ms,
-                           "profile": pfile if prof else None,
-                           "note": "%d algorithmic B/game written (final board, diff, plies); the kernel is "
-                                   "integer-VALU-bound, see 'valu'" % ROLLOUT_BYTES_PER_GAME}
-        if prof and "SQ_INSTS_VALU" in prof:
-            va = prof["SQ_INSTS_VALU"] / (kern_ms * 1e-3)
-            out["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s",
-                           "frac": va / VALU_PEAK_WINSTR, "instr_per_launch": prof["SQ_INSTS_VALU"],
-                           "busy_pmc": prof.get("valu_busy"), "clock_ghz_pmc": prof.get("clock_ghz")}
+        out.update(_bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist, barrier,
+                                  max_over_ranks, args.streams))
     else:
         out.update(_bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks))
 
@@ -230,6 +173,14 @@ def main():
         # rollout_16M, which runs the headline kernel at the headline grid and would
         # otherwise be averaged into the headline's per-launch profile figures
         skip = set(filter(None, os.environ.get("BENCH_SKIP", "").split(",")))
+        if args.workload in ("rollout", "greedy") and args.streams != 1 and "rollout_1stream" not in skip:
+            def serial():
+                r = _bench_rollout(torch, dist, dev, stream, args, policy, 1, 0, False, torch.cuda.synchronize,
+                                   lambda x: x, 1)
+                return {"metric": r["metric"] + ", one stream (launches serialized)", "value": r["value"],
+                        "unit": r["unit"], "ms_per_step": r["ms_per_step"], "launch_ms": r["roofline"]["launch_ms"],
+                        "valu_frac": r.get("valu", {}).get("frac")}
+            guarded("rollout_1stream", serial)
         if args.workload == "rollout" and "rollout_16M" not in skip:
             guarded("rollout_16M", lambda: _bench_rollout_big(ops, torch, dev, args))
         if args.workload != "greedy":
@@ -245,6 +196,137 @@ def main():
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.destroy_process_group()
+
+
+def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist, barrier, max_over_ranks,
+                   nstreams):
+    """Configs 3/4/5: K bench steps, each one oth_rollout launch over `games`
+    fresh games per GPU (+ the histogram all-reduce at N>1).  Steps are issued
+    round-robin on `nstreams` HIP streams, each with its own output buffers:
+    a launch's last batches (the per-launch tail, DESIGN.md §Rollout
+    scheduling) then share the CUs with the next step's first batches instead
+    of idling them.  Every step still plays all of its games; nstreams=1 is
+    the serialized figure."""
+    from subproc_amd import _lib
+    from subproc_amd._lib import HIST_BINS
+
+    n = args.games
+    hists = torch.zeros((args.warmup + args.steps, HIST_BINS), dtype=torch.int64, device=dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
+    bufs = [(torch.empty((n, 2), dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int8, device=dev),
+             torch.empty(n, dtype=torch.uint8, device=dev)) for _ in streams]
+    lib = _lib.load()
+    pid = 0 if policy == "random" else 1
+    pending = []
+    # per-launch events on the launch's own stream (the roofline's launch duration)
+    l0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    l1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def one_step(s, k=None):
+        # bench step s plays global game ids [(s*world + rank)*n, +n): fresh games every step
+        st = streams[s % nstreams]
+        fb, df, pl = bufs[s % nstreams]
+        h = hists[s]
+        if k is not None and LAUNCH_EVENTS:
+            l0[k].record(st)
+        _lib.check(lib.oth_rollout(None, None, args.seed, (s * world + rank) * n, pid, 10, fb.data_ptr(),
+                                   df.data_ptr(), pl.data_ptr(), None, h.data_ptr(), n, st.cuda_stream),
+                   "oth_rollout")
+        if k is not None and LAUNCH_EVENTS:
+            l1[k].record(st)
+        if use_dist and args.allreduce != "end":
+            # config 4: the one collective, ordered after this step's rollout on its stream.
+            # Async on RCCL's stream, so it overlaps the next steps (each step owns its
+            # histogram row); all are waited for inside the timed region.
+            with torch.cuda.stream(st):
+                work = dist.all_reduce(h, op=dist.ReduceOp.SUM, async_op=args.allreduce == "async")
+            if work is not None:
+                pending.append(work)
+
+    def drain():
+        while pending:
+            pending.pop().wait()
+
+    def fork():  # side streams start after everything issued so far on the main stream
+        e = torch.cuda.Event()
+        e.record(stream)
+        for st in streams[1:]:
+            st.wait_event(e)
+
+    def join():  # the main stream waits for the side streams
+        for st in streams[1:]:
+            e = torch.cuda.Event()
+            e.record(st)
+            stream.wait_event(e)
+
+    # clock pre-warm (untimed, local, no collective): the GPU ramps its clock
+    # over the first ~100 ms of work, longer than a few warmup steps take
+    scratch = torch.zeros(HIST_BINS, dtype=torch.int64, device=dev)
+    t_w = time.perf_counter()
+    while (time.perf_counter() - t_w) * 1e3 < args.prewarm_ms:
+        fb, df, pl = bufs[0]
+        _lib.check(lib.oth_rollout(None, None, args.seed, 1 << 52, pid, 10, fb.data_ptr(), df.data_ptr(),
+                                   pl.data_ptr(), None, scratch.data_ptr(), n, stream.cuda_stream), "oth_rollout")
+        torch.cuda.synchronize()
+    fork()
+    for s in range(args.warmup):
+        one_step(s)
+    join()
+    drain()
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    fork()
+    for k, s in enumerate(range(args.warmup, args.warmup + args.steps)):
+        one_step(s, k)
+    join()
+    if use_dist and args.allreduce == "end":
+        total = hists[args.warmup:].sum(0)
+        dist.all_reduce(total, op=dist.ReduceOp.SUM)
+        hists[args.warmup].copy_(total)
+        hists[args.warmup + 1:].zero_()
+    ev1.record(stream)
+    drain()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(t1 - t0)
+    step_ms = ev0.elapsed_time(ev1) / args.steps  # stream time per step (+ the all-reduce at N>1)
+    launch = sorted(l0[k].elapsed_time(l1[k]) for k in range(args.steps)) if LAUNCH_EVENTS else [step_ms]
+    launch_ms = sum(launch) / len(launch)
+    median_ms = launch[len(launch) // 2] if len(launch) % 2 else \
+        0.5 * (launch[len(launch) // 2 - 1] + launch[len(launch) // 2])
+    timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) when distributed
+    env_steps = int(timed[132])
+    games = n * world * args.steps
+    out = dict(metric="env-steps/sec (batched self-play)", value=env_steps / elapsed, unit="env-steps/s",
+               n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u64",
+               data="synthetic (games from the opening, counter-based RNG seed %#x)" % args.seed,
+               prewarm_ms=args.prewarm_ms,
+               config={"workload": "config%d: %s-policy self-play rollouts to terminal" %
+                       (3 if policy == "random" and world == 1 else 4 if policy == "random" else 5, policy),
+                       "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
+                       "streams": nstreams, "env_steps_per_game": env_steps / games})
+    # roofline: algorithmic bytes of one launch / that launch's duration (events on its stream)
+    achieved = n * ROLLOUT_BYTES_PER_GAME / (launch_ms * 1e-3) / 1e9
+    kname = "rollout_kernel<%d, false>" % pid
+    pfile, kernels = load_profile()
+    prof = profile_entry(kernels, kname) if n == 1 << 20 else None
+    out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": achieved / HBM_PEAK_GBS,
+                       "traffic": prof.get("hbm_bytes") if prof else None,
+                       "kernel": kname, "launch_ms": launch_ms, "launch_ms_median": median_ms,
+                       "step_ms": step_ms, "profile": pfile if prof else None,
+                       "note": "%d algorithmic B/game written (final board, diff, plies); the kernel is "
+                               "integer-VALU-bound, see 'valu'. launch_ms: one launch's duration; step_ms: "
+                               "stream time per step with %d launches in flight" % (ROLLOUT_BYTES_PER_GAME,
+                                                                                     nstreams)}
+    if prof and "SQ_INSTS_VALU" in prof:
+        # device-wide issue rate: a launch's instructions per step of stream time
+        va = prof["SQ_INSTS_VALU"] / (step_ms * 1e-3)
+        out["valu"] = valu_entry(kname, va, instr_per_launch=prof["SQ_INSTS_VALU"])
+    return out
 
 
 def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks, launches=None):
@@ -284,8 +366,7 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
                       "kernel": "step_kernel", "profile": pfile if prof else None}}
     if prof and "SQ_INSTS_VALU" in prof:
         va = prof["SQ_INSTS_VALU"] / (kern_ms * 1e-3)
-        r["valu"] = {"achieved": va, "peak": VALU_PEAK_WINSTR, "unit": "wave-instr/s", "frac": va / VALU_PEAK_WINSTR,
-                     "busy_pmc": prof.get("valu_busy")}
+        r["valu"] = valu_entry("step_kernel", va)
     return r
 
 

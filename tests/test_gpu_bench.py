@@ -1,0 +1,46 @@
+"""bench.py keeps the driver's JSON contract: a short run on one GPU prints one
+line with the required keys, and the multi-stream rollout steps count exactly
+the env-steps the games played (the histogram's ply total)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline"}
+
+
+def _run(extra, env_extra=None):
+    env = dict(os.environ, **(env_extra or {}))
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--games", "65536",
+                        "--no-secondary"] + extra, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("streams", [1, 2])
+def test_bench_rollout_line(streams):
+    out = _run(["--streams", str(streams)])
+    assert REQUIRED <= set(out)
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["config"]["streams"] == streams
+    assert out["unit"] == "env-steps/s" and out["value"] > 0
+    # 65536 random games average ~60.4 plies
+    assert 59.5 < out["config"]["env_steps_per_game"] < 61.5
+    rf = out["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["launch_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rollout_rccl_path_one_rank():
+    """The N>1 code path (RCCL barrier, per-step async histogram all-reduce on
+    each step's stream, max over ranks) at world size 1."""
+    out = _run(["--allreduce", "async"], {"BENCH_FORCE_DIST": "1", "RANK": "0", "LOCAL_RANK": "0",
+                                           "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                                           "MASTER_PORT": "29531"})
+    assert 59.5 < out["config"]["env_steps_per_game"] < 61.5

@@ -422,3 +422,42 @@ def test_rollout_captured_in_a_graph_replays_correctly():
         assert torch.equal(hist, ref.hist), k
         mid = ops.rollout(n, 9, 50, device=DEV)
         assert torch.equal(mid.hist, ref.hist), k
+
+
+def _high_mobility_boards(m, seed, iters=400):
+    """Hill-climb random boards (single-square mutations kept when Black's
+    mobility does not drop) to positions with 24..33 legal moves."""
+    rng = np.random.default_rng(seed)
+    occ = rng.integers(0, 2**64, m, dtype=np.uint64) & rng.integers(0, 2**64, m, dtype=np.uint64)
+    nb = np.stack([occ & ~rng.integers(0, 2**64, m, dtype=np.uint64), np.zeros(m, np.uint64)], 1)
+    nb[:, 1] = occ & ~nb[:, 0]
+    black = np.full(m, 1, np.uint8)
+    cur = np.bitwise_count(oracle.legal(nb, black)).astype(int)
+    for _ in range(iters):
+        bit = np.uint64(1) << rng.integers(0, 64, m).astype(np.uint64)
+        kind = rng.integers(0, 3, m)
+        nb2 = nb & ~bit[:, None]
+        nb2[kind == 1, 0] |= bit[kind == 1]
+        nb2[kind == 2, 1] |= bit[kind == 2]
+        m2 = np.bitwise_count(oracle.legal(nb2, black)).astype(int)
+        acc = m2 >= cur
+        nb[acc], cur[acc] = nb2[acc], m2[acc]
+    return nb, cur
+
+
+def test_greedy_eval_coop_overflow_fallback_vs_oracle():
+    """A wave whose children overflow the cooperative list (64 x 20 entries)
+    falls back to per-lane evaluation for that ply (othello.hip coop_choose):
+    start every game where the mover has >= 21 legal moves (64 x 21 > 1280), so
+    the first plies of every wave take the fallback and later plies the
+    cooperative path."""
+    from subproc_amd.params import DEFAULT_WEIGHTS
+    nb, mob = _high_mobility_boards(4096, 12)
+    assert mob.min() >= 21
+    tt = np.full(len(nb), 1, np.uint8)
+    for policy, pid, w in (("greedy", 1, None), ("eval", 2, DEFAULT_WEIGHTS)):
+        r = ops.rollout(len(nb), 8, 0, policy, 0, start=B(nb[:, 0], nb[:, 1]), start_turn=T(tt), record_moves=True,
+                        weights=w, device=DEV)
+        o = oracle.rollout(len(nb), 8, 0, pid, 0, start=nb, start_turn=tt, record_moves=True, weights=w)
+        assert (r.moves.cpu().numpy() == o["moves"]).all(), policy
+        assert (r.hist.cpu().numpy() == o["hist"]).all(), policy

@@ -7,7 +7,10 @@ Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
     streaming read: fetch_bytes_corrected = 2 * FETCH_SIZE * 1024 (an upper
     estimate for narrower accesses, which the guide leaves uncalibrated);
   * SQ_ACTIVE_INST_VALU counts quad-cycles; SQ_BUSY_CYCLES is summed over the
-    32 shader engines: VALU busy = 4 * ACTIVE_INST_VALU / (1024 SIMDs * BUSY/32).
+    32 shader engines: valu_busy = 4 * ACTIVE_INST_VALU / (1024 SIMDs * BUSY/32)
+    prices every VALU instruction at 4 cycles, so it can pass 1 when part of the
+    mix is plain VOP2 logic (~2.2 cycles); the mix-weighted ceiling is in
+    profiles/valu_mix.json (tools/valu_mix.py).
 """
 import collections
 import csv
@@ -80,8 +83,10 @@ def main(d):
                 e[c] = cs[c]
         if "SQ_ACTIVE_INST_VALU" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"] > 0:
             e["valu_busy"] = 4 * cs["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cs["SQ_BUSY_CYCLES"] / N_SE)
-        if "GRBM_GUI_ACTIVE" in cs and durs:
-            e["clock_ghz"] = cs["GRBM_GUI_ACTIVE"] / 8 / (sum(durs) / len(durs))
+        if "GRBM_GUI_ACTIVE" in cs:
+            # GPU cycles of the (serialized) PMC dispatch; not divided by the kernel-trace
+            # duration, which overlaps a neighbouring launch in the two-stream bench
+            e["gpu_cycles_pmc"] = cs["GRBM_GUI_ACTIVE"] / 8
         out["kernels"][f"{k}@{grid}"] = e
     out["kernel_stats"] = stats
     json.dump(out, sys.stdout, indent=1)

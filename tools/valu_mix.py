@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Static VALU instruction mix of each kernel's hot loop -> the issue ceiling
+bench.py prices the integer kernels against (profiles/valu_mix.json).
+
+CDNA4 SIMDs are 32 lanes wide: a wave64 VALU instruction can issue every 2
+cycles (MI355X_MICROARCH.md, cycle constants).  Measured on the box
+(tools/diag/valu_rate*.cpp, DESIGN.md §3 cost model), only plain VOP2 logic
+(v_and/or/xor/not/mov) streams at ~2.2 cycles; 64-bit shifts, v_bfi_b32,
+v_or3/bitop3, v_bcnt, v_cndmask, 32-bit shifts and SGPR-operand forms take ~4.
+So a kernel's ceiling is 1024 SIMDs x clock / (mean cycles over its mix).
+Unmeasured VOP2 forms (add/sub/min/max) are counted as fast, which raises the
+ceiling (the conservative side for a fraction-of-peak claim).
+
+The hot loop is the innermost LLVM loop (its header and every block tagged
+"in Loop: Header=<it>") holding the most VALU instructions; counts are static
+(every block once), so rarely-taken blocks inside the loop are included.
+    python tools/valu_mix.py [--asm file.s] > profiles/valu_mix.json
+"""
+import argparse
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAST = re.compile(r"^v_(and|or|xor|not|mov|add|sub|subrev|min|max)_(b32|u32|i32|b64)_e32$")
+FAST_CYC, SLOW_CYC = 2.2, 4.0
+KERNELS = {"rollout_kernel<0, false>": "rollout_kernelILi0ELb0E", "rollout_kernel<1, false>": "rollout_kernelILi1ELb0E",
+           "rollout_kernel<2, false>": "rollout_kernelILi2ELb0E", "step_kernel": "step_kernel"}
+
+
+def compile_asm():
+    out = os.path.join(tempfile.mkdtemp(), "othello.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-x", "hip", "--cuda-device-only", "-S",
+                    "-o", out, os.path.join(ROOT, "subproc_amd", "csrc", "othello.hip"),
+                    "-I", os.path.join(ROOT, "include")], check=True, capture_output=True)
+    return out
+
+
+def functions(lines):
+    cur, body = None, []
+    for ln in lines:
+        m = re.match(r"^(_Z\w+):", ln)
+        if m:
+            if cur:
+                yield cur, body
+            cur, body = m.group(1), []
+        elif cur:
+            body.append(ln)
+            if ln.startswith("\t.size\t" + cur) or ln.strip().startswith(".Lfunc_end"):
+                yield cur, body
+                cur = None
+    if cur:
+        yield cur, body
+
+
+def hot_loop_mix(body):
+    blocks, order, label = collections.defaultdict(list), [], None
+    header_of = {}
+    for ln in body:
+        m = re.match(r"^\.(LBB\w+):(.*)", ln)
+        if m:
+            label = m.group(1)
+            order.append(label)
+            h = re.search(r"Header=(BB\w+)", m.group(2))
+            if h:
+                header_of[label] = "L" + h.group(1)
+            if "Inner Loop Header" in m.group(2):
+                header_of[label] = label
+            continue
+        if label and re.match(r"^\s+; =>\s*This Inner Loop Header", ln):  # the comment on its own line
+            header_of[label] = label
+            continue
+        m = re.match(r"^\s+(v_[a-z0-9_]+)", ln)
+        if m and label:
+            blocks[label].append(m.group(1))
+    loops = collections.defaultdict(list)
+    for b, h in header_of.items():
+        loops[h].extend(blocks[b])
+    inner = {h: ops for h, ops in loops.items() if header_of.get(h) == h}
+    if not inner:
+        return None
+    h, ops = max(inner.items(), key=lambda kv: len(kv[1]))
+    fast = sum(1 for o in ops if FAST.match(o))
+    slow = len(ops) - fast
+    mean = (fast * FAST_CYC + slow * SLOW_CYC) / max(1, len(ops))
+    return {"loop_header": h, "valu": len(ops), "fast_vop2": fast, "slow": slow, "mean_cycles": round(mean, 3),
+            "top": collections.Counter(ops).most_common(8)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--asm")
+    a = p.parse_args()
+    path = a.asm or compile_asm()
+    lines = open(path).read().splitlines()
+    out = {"fast_cycles": FAST_CYC, "slow_cycles": SLOW_CYC, "simds": 1024, "clock_ghz": 2.4, "kernels": {}}
+    for name, body in functions(lines):
+        for k, pat in KERNELS.items():
+            if pat in name:
+                r = hot_loop_mix(body)
+                if r is None:  # no loop (elementwise kernels): the whole body
+                    ops = [m.group(1) for m in (re.match(r"^\s+(v_[a-z0-9_]+)", ln) for ln in body) if m]
+                    fast = sum(1 for o in ops if FAST.match(o))
+                    r = {"loop_header": None, "valu": len(ops), "fast_vop2": fast, "slow": len(ops) - fast,
+                         "mean_cycles": round((fast * FAST_CYC + (len(ops) - fast) * SLOW_CYC) / max(1, len(ops)), 3),
+                         "top": collections.Counter(ops).most_common(8)}
+                r["peak_winstr_s"] = out["simds"] * out["clock_ghz"] * 1e9 / r["mean_cycles"]
+                out["kernels"][k] = r
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()

@@ -81,12 +81,17 @@ def load_profile():
         return os.path.basename(files[-1]), json.load(f).get("kernels", {})
 
 
-def profile_entry(kernels, name, grid=None):
+def profile_entry(kernels, name, grid=None, largest=False):
+    """The profile entry of kernel `name` (at `grid` threads, or at its largest grid)."""
+    best = None
     for k, e in kernels.items():
         kn, g = k.rsplit("@", 1)
         if kn == name and (grid is None or int(g) == grid):
-            return e
-    return None
+            if not largest:
+                return e
+            if best is None or int(g) > best[0]:
+                best = (int(g), e)
+    return best[1] if best else None
 
 
 def parse():
@@ -183,9 +188,19 @@ def main():
             guarded("rollout_1stream", serial)
         if args.workload == "rollout" and "rollout_16M" not in skip:
             guarded("rollout_16M", lambda: _bench_rollout_big(ops, torch, dev, args))
+        def policy_line(pol):
+            a = argparse.Namespace(**vars(args))
+            a.steps, a.warmup, a.prewarm_ms = 10, 2, 0.0  # the GPU is warm by now
+            r = _bench_rollout(torch, dist, dev, stream, a, pol, 1, 0, False, torch.cuda.synchronize, lambda x: x,
+                               args.streams)
+            what = "greedy-mobility" if pol == "greedy" else "linear-eval (learner default weights)"
+            return {"metric": f"env-steps/sec ({what} self-play)", "value": r["value"], "unit": r["unit"],
+                    "games": args.games, "steps": a.steps, "streams": args.streams, "ms_per_step": r["ms_per_step"],
+                    "launch_ms": r["roofline"]["launch_ms"], "valu": r.get("valu")}
+
         if args.workload != "greedy":
-            guarded("greedy_1M", lambda: _bench_greedy(ops, torch, dev, stream, args))
-        guarded("eval_1M", lambda: _bench_greedy(ops, torch, dev, stream, args, policy="eval"))
+            guarded("greedy_1M", lambda: policy_line("greedy"))
+        guarded("eval_1M", lambda: policy_line("eval"))
         guarded("td_state_map", lambda: _bench_td(ops, torch, dev, args))
         out["secondary"] = sec
         try:
@@ -216,7 +231,21 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     bufs = [(torch.empty((n, 2), dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int8, device=dev),
              torch.empty(n, dtype=torch.uint8, device=dev)) for _ in streams]
     lib = _lib.load()
-    pid = 0 if policy == "random" else 1
+    pid = {"random": 0, "greedy": 1, "eval": 2}[policy]
+    wptr = None
+    if policy == "eval":
+        from subproc_amd.ops import _weights_ptr
+        from subproc_amd.params import DEFAULT_WEIGHTS
+
+        wptr = _weights_ptr(DEFAULT_WEIGHTS)  # the learner's default table
+
+    def launch(gid, fb, df, pl, h, st):
+        if policy == "eval":
+            return lib.oth_rollout_eval(None, None, args.seed, gid, 10, wptr, fb.data_ptr(), df.data_ptr(),
+                                        pl.data_ptr(), None, h.data_ptr(), n, st.cuda_stream)
+        return lib.oth_rollout(None, None, args.seed, gid, pid, 10, fb.data_ptr(), df.data_ptr(), pl.data_ptr(), None,
+                               h.data_ptr(), n, st.cuda_stream)
+
     pending = []
     # per-launch events on the launch's own stream (the roofline's launch duration)
     l0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -229,9 +258,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
         h = hists[s]
         if k is not None and LAUNCH_EVENTS:
             l0[k].record(st)
-        _lib.check(lib.oth_rollout(None, None, args.seed, (s * world + rank) * n, pid, 10, fb.data_ptr(),
-                                   df.data_ptr(), pl.data_ptr(), None, h.data_ptr(), n, st.cuda_stream),
-                   "oth_rollout")
+        _lib.check(launch((s * world + rank) * n, fb, df, pl, h, st), "rollout")
         if k is not None and LAUNCH_EVENTS:
             l1[k].record(st)
         if use_dist and args.allreduce != "end":
@@ -265,8 +292,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     t_w = time.perf_counter()
     while (time.perf_counter() - t_w) * 1e3 < args.prewarm_ms:
         fb, df, pl = bufs[0]
-        _lib.check(lib.oth_rollout(None, None, args.seed, 1 << 52, pid, 10, fb.data_ptr(), df.data_ptr(),
-                                   pl.data_ptr(), None, scratch.data_ptr(), n, stream.cuda_stream), "oth_rollout")
+        _lib.check(launch(1 << 52, fb, df, pl, scratch, stream), "rollout")
         torch.cuda.synchronize()
     fork()
     for s in range(args.warmup):
@@ -304,15 +330,15 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
                higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u64",
                data="synthetic (games from the opening, counter-based RNG seed %#x)" % args.seed,
                prewarm_ms=args.prewarm_ms,
-               config={"workload": "config%d: %s-policy self-play rollouts to terminal" %
-                       (3 if policy == "random" and world == 1 else 4 if policy == "random" else 5, policy),
+               config={"workload": "config%s: %s-policy self-play rollouts to terminal" %
+                       ({"random": "3" if world == 1 else "4", "greedy": "5", "eval": " §8f"}[policy], policy),
                        "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
                        "streams": nstreams, "env_steps_per_game": env_steps / games})
     # roofline: algorithmic bytes of one launch / that launch's duration (events on its stream)
     achieved = n * ROLLOUT_BYTES_PER_GAME / (launch_ms * 1e-3) / 1e9
     kname = "rollout_kernel<%d, false>" % pid
     pfile, kernels = load_profile()
-    prof = profile_entry(kernels, kname) if n == 1 << 20 else None
+    prof = profile_entry(kernels, kname, largest=True) if n == 1 << 20 else None
     out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK_GBS,
                        "traffic": prof.get("hbm_bytes") if prof else None,
@@ -416,23 +442,6 @@ def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):
     dt = time.perf_counter() - t0
     return {"metric": "env-steps/sec (random self-play, 16M games per launch)", "value": int(hist[132]) / dt,
             "unit": "env-steps/s", "games": games, "launches": reps, "ms_per_launch": dt / reps * 1e3}
-
-
-def _bench_greedy(ops, torch, dev, stream, args, policy="greedy"):
-    """config 5 (policy "greedy") or the eval-table policy (§8f row 2, default
-    learner weights): n games, 10 random plies, then the 1-ply policy."""
-    n = args.games
-    hist = torch.zeros(133, dtype=torch.int64, device=dev)
-    ops.rollout(n // 16, args.seed, 0, policy, 10, hist=hist, device=dev, want_boards=False)
-    torch.cuda.synchronize()
-    hist.zero_()
-    t0 = time.perf_counter()
-    ops.rollout(n, args.seed, 1 << 40, policy, 10, hist=hist, device=dev)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    what = "greedy-mobility" if policy == "greedy" else "linear-eval (learner default weights)"
-    return {"metric": f"env-steps/sec ({what} self-play)", "value": int(hist[132]) / dt,
-            "unit": "env-steps/s", "games": n, "ms": dt * 1e3}
 
 
 def _bench_td(ops, torch, dev, args, games=1 << 18):

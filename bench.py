@@ -156,9 +156,12 @@ def main():
         out.update(_bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist, barrier,
                                   max_over_ranks, args.streams))
     else:
-        out.update(_bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks))
+        out.update(_bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks,
+                               index0=rank * 65536))
 
-    if world == 1 and not args.no_secondary:  # secondary + cpu_baseline: rank 0 at N=1 only
+    # secondary + cpu_baseline: rank 0 at N=1 only (BENCH_FORCE_DIST=1 at N=1
+    # takes the N>1 branch below instead, so one GPU exercises it)
+    if world == 1 and not use_dist and not args.no_secondary:
         sec = {}
 
         def guarded(name, fn):
@@ -207,6 +210,16 @@ def main():
             out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
         except Exception as e:  # noqa: BLE001
             out["cpu_baseline"] = {"error": repr(e)}
+    elif use_dist and not args.no_secondary and args.workload != "step":
+        # N>1: config 2's step over synthetic mid-game positions on every rank
+        # (disjoint positions per rank, barrier + max-over-ranks timing), so the
+        # step's env-steps/s and HBM roofline are reported at 2/4/8 GPUs too.
+        # Not guarded: every rank must reach the same collectives.
+        out["secondary"] = {
+            "step_steady_16M": _bench_step(ops, torch, dev, stream, args, 1 << 24, world, barrier, max_over_ranks,
+                                           launches=10, index0=rank << 24),
+            "step_65536": _bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks,
+                                      launches=200, index0=rank * 65536)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_dist:
@@ -224,6 +237,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     the serialized figure."""
     from subproc_amd import _lib
     from subproc_amd._lib import HIST_BINS
+    from subproc_amd.dist import bench_game_id0
 
     n = args.games
     hists = torch.zeros((args.warmup + args.steps, HIST_BINS), dtype=torch.int64, device=dev)
@@ -258,7 +272,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
         h = hists[s]
         if k is not None and LAUNCH_EVENTS:
             l0[k].record(st)
-        _lib.check(launch((s * world + rank) * n, fb, df, pl, h, st), "rollout")
+        _lib.check(launch(bench_game_id0(s, rank, world, n), fb, df, pl, h, st), "rollout")
         if k is not None and LAUNCH_EVENTS:
             l1[k].record(st)
         if use_dist and args.allreduce != "end":
@@ -355,12 +369,13 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     return out
 
 
-def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks, launches=None):
-    """config 2: oth_step over n reachable mid-game positions (inputs resident in HBM)."""
+def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks, launches=None, index0=0):
+    """config 2: oth_step over n reachable mid-game positions (inputs resident in
+    HBM); at N>1 each rank steps its own positions [index0, index0 + n)."""
     from subproc_amd import _lib
 
     lib = _lib.load()
-    pos = ops.sample_midgame(n, args.seed, index0=0, device=dev)
+    pos = ops.sample_midgame(n, args.seed, index0=index0, device=dev)
     bo = torch.empty_like(pos.boards)
     to = torch.empty_like(pos.turn)
     fl = torch.empty(n, dtype=torch.int64, device=dev)
@@ -386,7 +401,7 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
     pfile, kernels = load_profile()
     prof = profile_entry(kernels, "step_kernel", n)
     r = {"metric": "env-steps/sec (batched step)", "value": steps / elapsed, "unit": "env-steps/s",
-         "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
+         "n_gpus": world, "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
          "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("hbm_bytes") if prof else None,
                       "kernel": "step_kernel", "profile": pfile if prof else None}}

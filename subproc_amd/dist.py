@@ -20,6 +20,14 @@ def shard_range(total, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
+def bench_game_id0(step, rank, world, n):
+    """First global game id of bench step `step` on `rank` (bench.py): step s
+    plays ids [(s*world + r)*n, +n) on rank r, so every (step, rank) pair gets
+    fresh, disjoint games and the ids of steps 0..K-1 over all ranks tile
+    [0, K*world*n) exactly (tests/test_dist.py)."""
+    return (step * world + rank) * n
+
+
 def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None, rollout_fn=None, device=None,
                     game_id_base=0):
     """Play `total_games` games split over the ranks of `group`; returns

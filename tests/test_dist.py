@@ -10,7 +10,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from subproc_amd.dist import hist_summary, rollout_sharded, shard_range
+from subproc_amd.dist import bench_game_id0, hist_summary, rollout_sharded, shard_range
 
 
 def _oracle_fn(n, seed, game_id0, policy, n_random, hist):
@@ -26,19 +26,48 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, total, seed, out):
+def _worker(rank, world, port, total, seed, out, bench_steps=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    hist, local = rollout_sharded(total, seed, rollout_fn=_oracle_fn, device="cpu")
+    if bench_steps:
+        # bench.py's schedule: K steps of `total` games per rank, ids from
+        # bench_game_id0, one histogram per step, summed and all-reduced once
+        hist = torch.zeros(oracle.HIST_BINS, dtype=torch.int64)
+        for s in range(bench_steps):
+            _oracle_fn(total, seed, bench_game_id0(s, rank, world, total), "random", 10, hist)
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+        local = bench_steps * total
+    else:
+        hist, local = rollout_sharded(total, seed, rollout_fn=_oracle_fn, device="cpu")
     out[rank] = (hist.numpy().copy(), local)
     dist.destroy_process_group()
 
 
-def _run(world, total, seed):
+def _run(world, total, seed, bench_steps=0):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), total, seed, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), total, seed, out, bench_steps), nprocs=world, join=True)
     return dict(out)
+
+
+def test_bench_game_ids_tile_the_run():
+    """bench.py step s on rank r plays [(s*world + r)*n, +n): over K steps and all
+    ranks the ids are disjoint and cover [0, K*world*n) exactly."""
+    n, K = 5, 4
+    for world in (1, 2, 4, 8):
+        ids = [g for s in range(K) for r in range(world)
+               for g in range(bench_game_id0(s, r, world, n), bench_game_id0(s, r, world, n) + n)]
+        assert sorted(ids) == list(range(K * world * n))
+
+
+def test_world2_bench_schedule_equals_single_process():
+    """The bench's N>1 reduction (per-step shards, one all-reduce at the end) ==
+    one process over the same global ids, bit for bit."""
+    n, K, seed = 37, 3, 0x5EED
+    res = _run(2, n, seed, bench_steps=K)
+    ref = oracle.rollout(2 * K * n, seed, 0)["hist"]
+    for rank in (0, 1):
+        np.testing.assert_array_equal(res[rank][0], ref)
 
 
 def test_shard_range_partitions():

@@ -13,10 +13,11 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "vs_baseline", "dtype", "data", "config", "roofline"}
 
 
-def _run(extra, env_extra=None):
+def _run(extra, env_extra=None, secondary=False):
     env = dict(os.environ, **(env_extra or {}))
     r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--games", "65536",
-                        "--no-secondary"] + extra, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+                        "--prewarm-ms", "0"] + ([] if secondary else ["--no-secondary"]) + extra,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -44,3 +45,17 @@ def test_bench_rollout_rccl_path_one_rank():
                                            "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
                                            "MASTER_PORT": "29531"})
     assert 59.5 < out["config"]["env_steps_per_game"] < 61.5
+
+
+@pytest.mark.gpu
+def test_bench_dist_secondary_step_lines_one_rank():
+    """The N>1 secondary lines (config 2's step over each rank's own mid-game
+    positions, barrier + max-over-ranks timing) at world size 1."""
+    out = _run([], {"BENCH_FORCE_DIST": "1", "RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1",
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29532"}, secondary=True)
+    sec = out["secondary"]
+    assert set(sec) == {"step_steady_16M", "step_65536"}
+    for name, n in (("step_steady_16M", 1 << 24), ("step_65536", 65536)):
+        s = sec[name]
+        assert s["n_gpus"] == 1 and s["batch"] == n and s["value"] > 0
+        assert 0 < s["roofline"]["frac"] < 1

@@ -268,8 +268,10 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
         legal_next[i] = valid_turn ? moves(nP, nO) : 0ull;
     }
     if (boards_out) {
+        // (an invalid turn leaves P = b.y, O = b.x untouched and black false, so
+        // this already writes the input board back)
         const u64 nb = black ? P : O, nw = black ? O : P;
-        reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(valid_turn ? nb : b.x, valid_turn ? nw : b.y);
+        reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(nb, nw);
     }
     if (turn_out) turn_out[i] = (uint8_t)t_out;
     if (flips_out) flips_out[i] = f;
@@ -284,8 +286,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, cons
                                                       uint8_t* __restrict__ nturn, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    step_board(i, reinterpret_cast<const ulonglong2*>(boards_in)[i], turn_in[i], move[i], boards_out, turn_out,
-               flips_out, legal_next, ret_out, nturn);
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
+    const u32 t = turn_in[i], mvc = move[i];
+    // all three loads in flight together: without this hipcc sinks the move
+    // load into the valid-turn branch, a second dependent HBM round trip per wave
+    asm volatile("" ::"v"(t), "v"(mvc));
+    step_board(i, b, t, mvc, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
 }
 
 __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ boards, uint8_t* __restrict__ nb,

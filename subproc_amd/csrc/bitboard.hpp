@@ -144,11 +144,17 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
         tab[e] = row < 3 ? r : rev64(r);
     }
 }
-__device__ __forceinline__ u32 bitop3_and3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80); }
-__device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) {
-    return ((u64)bitop3_and3((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32)) << 32) |
-           bitop3_and3((u32)a, (u32)b, (u32)c);
+// any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the truth
+// table indexed by (a, b, c) bits: 0x80 = a & b & c, 0x20 = a & ~b & c (both
+// read the same under either operand order of the index).
+template <int TT>
+__device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
+    // (the builtin returns int: take both halves as u32, no sign extension)
+    const u32 hi = (u32)__builtin_amdgcn_bitop3_b32((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32), TT);
+    const u32 lo = (u32)__builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, TT);
+    return ((u64)hi << 32) | lo;
 }
+__device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bitop3<0x80>(a, b, c); }
 __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
     const u64 x = andn(R, A);
     return and3(R, A, x - 1);
@@ -163,6 +169,68 @@ __device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const Position& s, con
     f |= run_prefix(tab[2 * 64 + sq], s.A[7]);
     fr = or3(fr, run_prefix(tab[3 * 64 + sq], rev64(s.A[2])), run_prefix(tab[4 * 64 + sq], rev64(s.A[4])));
     fr |= run_prefix(tab[5 * 64 + sq], rev64(s.A[6]));
+    return f | rev64(fr);
+}
+
+// ---------------------------------------------------------------------------
+// Flips of one move without run sets (the single-step kernel, where the mover's
+// analysis is not otherwise needed).  Along a ray R leaving the move in
+// increasing bit order, the carry of (O | ~R) + (first square of R) ripples
+// through the opponent discs at the start of the ray and the non-ray bits
+// between them, and stops on the first ray square that is not an opponent
+// disc, which it sets.  The opponent squares it cleared are the run; they flip
+// iff the stop square holds a P disc.  A run that reaches the edge carries out
+// of the ray: no stop square, no flips.  An off-board ray is empty (the table
+// row is 0), so nothing is selected from it.
+__device__ __forceinline__ u64 ray_flips(u64 first, u64 R, u64 P, u64 O) {
+    const u64 sum = bfi(R, O, ~0ull) + first;   // (O | ~R) + first
+    const u64 run = bitop3<0x20>(R, sum, O);    // R & ~sum & O
+    return and3(sum, R, P) ? run : 0ull;        // stop square is P
+}
+
+// The ray table of ray_table_init as data, so a kernel can copy it into LDS
+// with one 16-byte load per thread instead of computing it.
+struct RayTable {
+    u64 r[kRayRows * 64];
+};
+constexpr u64 ray_from_c(int sq, int dx, int dy) {
+    u64 r = 0;
+    for (int x = (sq & 7) + dx, y = (sq >> 3) + dy; x >= 0 && x < 8 && y >= 0 && y < 8; x += dx, y += dy)
+        r |= 1ull << (x + 8 * y);
+    return r;
+}
+constexpr u64 rev64_c(u64 x) {
+    u64 r = 0;
+    for (int i = 0; i < 64; i++) r |= ((x >> i) & 1ull) << (63 - i);
+    return r;
+}
+constexpr RayTable make_ray_table() {
+    RayTable t{};
+    const int dx[kRayRows] = {0, 1, -1, 0, -1, 1}, dy[kRayRows] = {1, 1, 1, -1, -1, -1};
+    for (int row = 0; row < kRayRows; row++)
+        for (int sq = 0; sq < 64; sq++) {
+            const u64 r = ray_from_c(sq, dx[row], dy[row]);
+            t.r[row * 64 + sq] = row < 3 ? r : rev64_c(r);
+        }
+    return t;
+}
+__constant__ RayTable kRayTable = make_ray_table();
+
+// flips of the move on empty square sq (Board.put's count is their popcount,
+// board.py:161-174); 0 when nothing is flanked.  Horizontal runs by the carry
+// on the inner files (no ray mask needed), the six others by ray_flips; rays
+// leaving in decreasing bit order on the bit-reversed board (tab rows 3..5).
+__device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O, const u64* tab) {
+    const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
+    const u64 rP = rev64(P), rO = rev64(O);
+    const u64 Oi = O & INNER_FILES, rOi = rO & INNER_FILES;
+    const u64 se = Oi + (mv << 1), sw = rOi + (rmv << 1);
+    u64 f = (se & P) ? andn(Oi, se) : 0ull;
+    u64 fr = (sw & rP) ? andn(rOi, sw) : 0ull;
+    f = or3(f, ray_flips(mv << 8, tab[0 * 64 + sq], P, O), ray_flips(mv << 9, tab[1 * 64 + sq], P, O));
+    f |= ray_flips(mv << 7, tab[2 * 64 + sq], P, O);
+    fr = or3(fr, ray_flips(rmv << 8, tab[3 * 64 + sq], rP, rO), ray_flips(rmv << 9, tab[4 * 64 + sq], rP, rO));
+    fr |= ray_flips(rmv << 7, tab[5 * 64 + sq], rP, rO);
     return f | rev64(fr);
 }
 

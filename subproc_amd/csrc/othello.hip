@@ -235,9 +235,10 @@ __global__ __launch_bounds__(kBlock) void legal_kernel(const u64* __restrict__ b
 }
 
 // one board of the step (board.py:192-209 semantics, see include/othello.h)
-__device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 mvc, u64* boards_out, uint8_t* turn_out,
-                                           u64* __restrict__ flips_out, u64* __restrict__ legal_next,
-                                           int8_t* __restrict__ ret_out, uint8_t* __restrict__ nturn) {
+__device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 mvc, const u64* rays, u64* boards_out,
+                                           uint8_t* turn_out, u64* __restrict__ flips_out,
+                                           u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
+                                           uint8_t* __restrict__ nturn) {
     const bool valid_turn = (t == OTH_BLACK) | (t == OTH_WHITE);
     const bool black = t == OTH_BLACK;
     u64 P = black ? b.x : b.y;
@@ -250,7 +251,7 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
         } else if (mvc < 64) {
             const u64 mv = 1ull << mvc;
             if (!((P | O) & mv)) {
-                f = flips_tested(mv, P, O);
+                f = flips_carry(mvc, P, O, rays);
                 if (f) {
                     r = __popcll(f);
                     P |= f | mv;
@@ -284,14 +285,26 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, cons
                                                       uint8_t* turn_out, u64* __restrict__ flips_out,
                                                       u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
                                                       uint8_t* __restrict__ nturn, int64_t n) {
+    __shared__ u64 rays[kRayRows * 64];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
-    const u32 t = turn_in[i], mvc = move[i];
-    // all three loads in flight together: without this hipcc sinks the move
-    // load into the valid-turn branch, a second dependent HBM round trip per wave
+    const bool in = i < n;
+    ulonglong2 b = make_ulonglong2(0, 0);
+    u32 t = 0, mvc = 0;
+    if (in) {
+        b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
+        t = turn_in[i];
+        mvc = move[i];
+    }
+    // the ray table (3 KiB, L2-resident) rides along with the board loads
+    static_assert(kRayRows * 32 <= kBlock, "one 16-byte table piece per thread");
+    if (threadIdx.x < kRayRows * 32)
+        reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = reinterpret_cast<const ulonglong2*>(kRayTable.r)[threadIdx.x];
+    // all loads in flight together: without this hipcc sinks the move load into
+    // the valid-turn branch, a second dependent HBM round trip per wave
     asm volatile("" ::"v"(t), "v"(mvc));
-    step_board(i, b, t, mvc, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
+    __syncthreads();
+    if (!in) return;
+    step_board(i, b, t, mvc, rays, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
 }
 
 __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ boards, uint8_t* __restrict__ nb,

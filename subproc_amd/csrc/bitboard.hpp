@@ -160,15 +160,31 @@ __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
     return and3(R, A, x - 1);
 }
 
-// flips of the move at square sq (bit mv): horizontal rays by carry (as in
-// analyse), the other six by the ray tables; A sets from analyse(P, O).
-__device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const Position& s, const u64* tab) {
-    u64 f = east_run(mv, s.Oi) & s.A[1];
-    u64 fr = east_run(rev64(mv), s.rOi) & rev64(s.A[0]);  // west, in reversed space
-    f = or3(f, run_prefix(tab[0 * 64 + sq], s.A[3]), run_prefix(tab[1 * 64 + sq], s.A[5]));
-    f |= run_prefix(tab[2 * 64 + sq], s.A[7]);
-    fr = or3(fr, run_prefix(tab[3 * 64 + sq], rev64(s.A[2])), run_prefix(tab[4 * 64 + sq], rev64(s.A[4])));
-    fr |= run_prefix(tab[5 * 64 + sq], rev64(s.A[6]));
+// The run sets flips_rays reads, in the orientation it reads them: the runs
+// leaving a move in increasing bit order lie in A[1], A[3], A[5], A[7] (the
+// opposite directions' runs, as analyse gives them), those leaving in
+// decreasing order in A[0], A[2], A[4], A[6], kept bit-reversed.  The 1-ply
+// policies build this once per parent and share it among its children.
+struct RunSets {
+    u64 A1, A3, A5, A7, rA0, rA2, rA4, rA6;
+};
+__device__ __forceinline__ RunSets run_sets(const Position& s) {
+    return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), rev64(s.A[2]), rev64(s.A[4]), rev64(s.A[6])};
+}
+
+// flips of the move at square sq (bit mv).  Horizontal: the run of A[1] that
+// starts right east of the move is exactly its east flips (an A[1] run is
+// attached to a P disc on its far side and bounded by the empty move square on
+// this side; A runs lie on the inner files, so the carry never leaves the
+// row): one add, as east_run.  West the same on the reversed board with A[0].
+// The other six by the ray tables (run_prefix).
+__device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, const u64* tab) {
+    u64 f = east_run(mv, r.A1);
+    u64 fr = east_run(rev64(mv), r.rA0);  // west, in reversed space
+    f = or3(f, run_prefix(tab[0 * 64 + sq], r.A3), run_prefix(tab[1 * 64 + sq], r.A5));
+    f |= run_prefix(tab[2 * 64 + sq], r.A7);
+    fr = or3(fr, run_prefix(tab[3 * 64 + sq], r.rA2), run_prefix(tab[4 * 64 + sq], r.rA4));
+    fr |= run_prefix(tab[5 * 64 + sq], r.rA6);
     return f | rev64(fr);
 }
 

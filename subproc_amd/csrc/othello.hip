@@ -102,7 +102,7 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // first in puttables order).  A child's score is a key whose minimum is the
 // choice: (score << 6) | square.
 template <int POLICY>
-__device__ __forceinline__ u32 child_key(u64 P, u64 O, const Position& s, u32 sq, const u64* rays, const int* w_tab) {
+__device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab) {
     const u64 mv = 1ull << sq;
     const u64 f = flips_rays(sq, mv, s, rays);
     const u64 P2 = P | f | mv, O2 = andn(O, f);
@@ -118,9 +118,10 @@ __device__ __forceinline__ u32 child_key(u64 P, u64 O, const Position& s, u32 sq
 
 // one lane alone over its own children (w_tab: the mover's eval table)
 template <int POLICY>
-__device__ __forceinline__ u32 lane_choose(const Position& s, u64 P, u64 O, const u64* rays, const int* w_tab) {
+__device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, const u64* rays, const int* w_tab) {
     u32 best = 0xFFFFFFFFu;
-    u64 legal = s.legal;
+    u64 legal = pos.legal;
+    const RunSets s = run_sets(pos);
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         legal &= legal - 1;
@@ -139,7 +140,7 @@ __device__ __forceinline__ u32 lane_choose(const Position& s, u64 P, u64 O, cons
 // lane_choose for that ply (only possible from unusual start positions).
 constexpr int kCoopCap = 64 * 20;  // children per wave per ply (mean mobility ~8.4)
 struct CoopWave {
-    u64 rec[64][10];          // parent lane: P, O, run sets A[0..7]
+    u64 rec[64][10];          // parent lane: P, O, its RunSets (8 words)
     uint16_t list[kCoopCap];  // (parent lane << 8) | (parent plays White) << 6 | square
     u32 best[64];
     u32 total;
@@ -148,13 +149,11 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, Position& s) {
+static_assert(sizeof(RunSets) == 8 * sizeof(u64), "parent record: P, O, RunSets");
+__device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, RunSets& s) {
     P = r[0];
     O = r[1];
-#pragma unroll
-    for (int d = 0; d < 8; d++) s.A[d] = r[2 + d];
-    s.Oi = O & INNER_FILES;
-    s.rOi = rev64(s.Oi);
+    s = *reinterpret_cast<const RunSets*>(r + 2);
 }
 // w_s: the two eval tables (Black's, then White's, kEvalTable ints each)
 template <int POLICY>
@@ -164,8 +163,7 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 side, const Position& po
         u64* r = cw.rec[lane];
         r[0] = P;
         r[1] = O;
-#pragma unroll
-        for (int d = 0; d < 8; d++) r[2 + d] = pos.A[d];
+        *reinterpret_cast<RunSets*>(r + 2) = run_sets(pos);  // reversed once per parent, not per child
         cw.best[lane] = 0xFFFFFFFFu;
         const u32 cnt = (u32)__popcll(pos.legal);
         u32 off = atomicAdd(&cw.total, cnt);
@@ -191,7 +189,7 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 side, const Position& po
                 const u32 e = cw.list[c];
                 const u32 par = e >> 8;
                 u64 Pp, Op;
-                Position ps;
+                RunSets ps;
                 load_parent(cw.rec[par], Pp, Op, ps);
                 atomicMin(&cw.best[par],
                           child_key<POLICY>(Pp, Op, ps, e & 63u, rays, w_s + ((e & 64u) ? kEvalTable : 0)));
@@ -452,7 +450,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
                 const u64 mv = 1ull << sq;
-                const u64 f = flips_rays(sq, mv, pos, rays);
+                const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                 if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                 const u64 np = andn(O, f);
                 O = P | f | mv;
@@ -513,7 +511,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 if (moving) {
                     const u64 mv = 1ull << sq;
-                    const u64 f = flips_rays(sq, mv, pos, rays);
+                    const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                     const u64 np = andn(O, f);
                     O = P | f | mv;

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kBlock, 4) void split_kernel(u64 seed_state, u64 ga
             }
             const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
             const u64 mv = 1ull << sq;
-            const u64 f = flips_rays(sq, mv, pos, rays);
+            const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
             const u64 np = andn(O, f);
             O = P | f | mv;
             P = np;

@@ -411,52 +411,59 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
 
         // ---- play the batch: one env-step per active lane per iteration
         if constexpr (POLICY == OTH_POLICY_RANDOM) {
-            // (kept separate: this exact loop is the measured config-3 kernel)
-            while (__ballot(active)) {
+            // (kept separate: this exact loop is the measured config-3 kernel).  A
+            // plain divergent loop: a lane leaves it with `break` at its terminal
+            // and the loop runs while any lane is left, on the exec mask alone
+            // (no per-iteration ballot).  The side to move is not tracked: P is
+            // side0's discs iff ply is even.  A pass is counted when it is
+            // handed over and uncounted at a terminal, so the common path only
+            // adds 1 to ply.
+            const u32 side0 = side;
+            if (active) {
+                for (;;) {
 #ifdef OTH_DIAG
-                diag_iters++;
+                    diag_iters++;
 #endif
-                if (!active) continue;
-                Position pos;
-                analyse(P, O, pos);
-                const u64 legal = pos.legal;
-                if (legal == 0) {
-                    if (passed) {
-                        // terminal: both sides without a legal move (board.py:57-58)
-                        const u64 bl = side == OTH_BLACK ? P : O, wh = side == OTH_BLACK ? O : P;
-                        const int d = __popcll(bl) - __popcll(wh);
-                        if (a.final_boards) reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
-                        if (a.diff) a.diff[g] = (int8_t)d;
-                        if (a.plies) a.plies[g] = (uint8_t)ply;
-                        atomicAdd(&hist_s[d + 64], 1ull);
-                        atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
-                        plies_sum += ply;
-                        active = false;
-                    } else {
-                        // the mover must pass: hand the move over tentatively; the pass
-                        // is counted once the other side turns out to have a move
+                    Position pos;
+                    analyse(P, O, pos);
+                    const u64 legal = pos.legal;
+                    if (legal == 0) {
+                        if (passed) {
+                            // terminal: both sides without a legal move (board.py:57-58);
+                            // the pass handed over just before is not an env-step
+                            const bool p_black = (side0 == OTH_BLACK) == ((ply & 1u) == 0u);
+                            ply--;
+                            if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
+                            const u64 bl = p_black ? P : O, wh = p_black ? O : P;
+                            const int d = __popcll(bl) - __popcll(wh);
+                            if (a.final_boards)
+                                reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
+                            if (a.diff) a.diff[g] = (int8_t)d;
+                            if (a.plies) a.plies[g] = (uint8_t)ply;
+                            atomicAdd(&hist_s[d + 64], 1ull);
+                            atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
+                            plies_sum += ply;
+                            break;
+                        }
+                        // the mover must pass ('PS'): hand the move over
+                        if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
                         passed = true;
                         const u64 t = P;
                         P = O;
                         O = t;
-                        side ^= 3u;
+                        ply++;
+                        continue;
                     }
-                    continue;
-                }
-                if (passed) {
-                    if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
-                    ply++;
                     passed = false;
+                    const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
+                    const u64 mv = 1ull << sq;
+                    const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
+                    if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
+                    const u64 np = andn(O, f);
+                    O = P | f | mv;
+                    P = np;
+                    ply++;
                 }
-                const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
-                const u64 mv = 1ull << sq;
-                const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
-                if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
-                const u64 np = andn(O, f);
-                O = P | f | mv;
-                P = np;
-                side ^= 3u;
-                ply++;
             }
         } else {
             while (__ballot(active)) {

@@ -34,6 +34,16 @@ __device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return (m & a) | (~m &
 __device__ __forceinline__ u64 andn(u64 a, u64 b) { return a & ~b; }
 __device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return a | b | c; }
 
+// any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the truth
+// table indexed by (a, b, c) bits: 0x80 = a & b & c, 0x20 = a & ~b & c, 0x04 = ~a & b & ~c
+// (each reads the same under either operand order of the index).
+template <int TT>
+__device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
+    // (the builtin returns int: take both halves as u32, no sign extension)
+    const u32 hi = (u32)__builtin_amdgcn_bitop3_b32((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32), TT);
+    const u32 lo = (u32)__builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, TT);
+    return ((u64)hi << 32) | lo;
+}
 template <int S, bool L>
 __device__ __forceinline__ u64 sh(u64 x) {
     return L ? (x << S) : (x >> S);
@@ -112,7 +122,7 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     m = or3(m, sh<9, false>(s.A[5]), sh<7, true>(s.A[6]));
     m |= sh<7, false>(s.A[7]);
     s.reach = m;
-    s.legal = andn(m, P | O);
+    s.legal = bitop3<0x04>(P, m, O);  // ~P & m & ~O: one v_bitop3_b32 per half
 }
 
 // ---------------------------------------------------------------------------
@@ -143,16 +153,6 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
         const u64 r = ray_from(sq, dx[row], dy[row]);
         tab[e] = row < 3 ? r : rev64(r);
     }
-}
-// any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the truth
-// table indexed by (a, b, c) bits: 0x80 = a & b & c, 0x20 = a & ~b & c (both
-// read the same under either operand order of the index).
-template <int TT>
-__device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
-    // (the builtin returns int: take both halves as u32, no sign extension)
-    const u32 hi = (u32)__builtin_amdgcn_bitop3_b32((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32), TT);
-    const u32 lo = (u32)__builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, TT);
-    return ((u64)hi << 32) | lo;
 }
 __device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bitop3<0x80>(a, b, c); }
 __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {

@@ -214,6 +214,37 @@ def test_every_code_random_boards_vs_oracle():
         assert (getattr(res, k).cpu().numpy() == ores[k]).all(), k
 
 
+def test_every_code_all_densities_vs_oracle():
+    """Every (board, code, side) triple over boards from nearly empty to nearly
+    full (runs reaching the edges, long runs, rays blocked by either colour):
+    the step's carry-along-the-ray flips and the next mover's legal mask."""
+    rng = np.random.default_rng(11)
+    per = 1024
+    parts = []
+    for k in (1, 2, 3, 4, 6):  # occupancy 1 - 2^-k: 50% ... 98%
+        occ = np.full(per, ~np.uint64(0), np.uint64)
+        for _ in range(k):
+            occ &= ~rng.integers(0, 2**64, per, dtype=np.uint64)
+        parts.append(~occ)
+    occ = np.concatenate(parts + [rng.integers(0, 2**64, per, dtype=np.uint64) & rng.integers(0, 2**64, per,
+                                                                                              dtype=np.uint64)])
+    col = rng.integers(0, 2**64, len(occ), dtype=np.uint64)
+    black, white = occ & col, occ & ~col
+    n = len(occ) * 65
+    nb = np.repeat(np.stack([black, white], 1), 65, axis=0)
+    mv = np.tile(np.arange(65, dtype=np.uint8), len(occ))
+    boards = B(nb[:, 0], nb[:, 1])
+    for turn in (1, 2):
+        tt = np.full(n, turn, np.uint8)
+        r = ops.step(boards, T(tt), T(mv))
+        o = oracle.step(nb, tt, mv)
+        assert (U(r.flips) == o["flips"]).all(), turn
+        assert (U(r.boards) == o["boards"]).all(), turn
+        assert (U(r.legal_next) == o["legal_next"]).all(), turn
+        assert (r.ret.cpu().numpy() == o["ret"]).all(), turn
+        assert (r.turn.cpu().numpy() == o["turn"]).all(), turn
+
+
 def test_rollout_random_65536_vs_oracle():
     n = 65536
     r = ops.rollout(n, 0x5EED, 0, device=DEV)

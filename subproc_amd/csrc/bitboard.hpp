@@ -9,7 +9,8 @@
 //   * Kogge-Stone propagators are computed once per position and shared between
 //     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S);
 //   * the chosen move's flips come from per-square ray tables in LDS and the
-//     run sets of the analysis (flips_rays), not from more fills.
+//     run sets of the analysis (flips_rays), not from more fills; without run
+//     sets (the single step) from one carry along each ray (flips_carry).
 //
 // Square sq = x + 8*y (board.py:74-81); rays of board.py:9-17 as shifts:
 //   +1 R (x+1), +8 D (y+1), +9 RD, +7 LD   and their opposites -1 L, -8 U, -9 LU, -7 RU.
@@ -196,57 +197,51 @@ __device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, cons
 // between them, and stops on the first ray square that is not an opponent
 // disc, which it sets.  The opponent squares it cleared are the run; they flip
 // iff the stop square holds a P disc.  A run that reaches the edge carries out
-// of the ray: no stop square, no flips.  An off-board ray is empty (the table
-// row is 0), so nothing is selected from it.
+// of the ray: no stop square, no flips.  An off-board ray is empty, so nothing
+// is selected from it.
 __device__ __forceinline__ u64 ray_flips(u64 first, u64 R, u64 P, u64 O) {
     const u64 sum = bfi(R, O, ~0ull) + first;   // (O | ~R) + first
     const u64 run = bitop3<0x20>(R, sum, O);    // R & ~sum & O
     return and3(sum, R, P) ? run : 0ull;        // stop square is P
 }
 
-// The ray table of ray_table_init as data, so a kernel can copy it into LDS
-// with one 16-byte load per thread instead of computing it.
-struct RayTable {
-    u64 r[kRayRows * 64];
-};
-constexpr u64 ray_from_c(int sq, int dx, int dy) {
-    u64 r = 0;
-    for (int x = (sq & 7) + dx, y = (sq >> 3) + dy; x >= 0 && x < 8 && y >= 0 && y < 8; x += dx, y += dy)
-        r |= 1ull << (x + 8 * y);
-    return r;
+// The six table rays of one square computed in registers (same rows as
+// ray_table_init): a shifted line pattern, masked to the files the ray can
+// reach.  Rows 3..5 are the decreasing rays in the bit-reversed layout, where
+// the square is 63 - sq and a file mask is the mirror (rev64) of its normal
+// counterpart.  ~20 VALU; the single-step kernel uses this instead of an LDS
+// table, whose per-block copy and barrier cost more than that
+// (tools/diag/launch_floor.py, step_ab.py).
+__device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
+    constexpr u64 ONES = 0x0101010101010101ull;
+    const u32 x = sq & 7u, rsq = sq ^ 63u;
+    const u64 le = (ONES << (x + 1)) - ONES;  // files <= x (x = 7: all)
+    const u64 lt = (ONES << x) - ONES;        // files < x
+    R[0] = 0x0101010101010100ull << sq;                            // +8
+    R[1] = andn(0x8040201008040200ull << sq, le);                  // +9: files > x
+    R[2] = (0x0002040810204080ull << sq) & lt;                     // +7: files < x
+    R[3] = 0x0101010101010100ull << rsq;                           // -8
+    R[4] = (0x8040201008040200ull << rsq) & rev64(lt);             // -9: normal files < x
+    R[5] = andn(0x0002040810204080ull << rsq, rev64(le));          // -7: normal files > x
 }
-constexpr u64 rev64_c(u64 x) {
-    u64 r = 0;
-    for (int i = 0; i < 64; i++) r |= ((x >> i) & 1ull) << (63 - i);
-    return r;
-}
-constexpr RayTable make_ray_table() {
-    RayTable t{};
-    const int dx[kRayRows] = {0, 1, -1, 0, -1, 1}, dy[kRayRows] = {1, 1, 1, -1, -1, -1};
-    for (int row = 0; row < kRayRows; row++)
-        for (int sq = 0; sq < 64; sq++) {
-            const u64 r = ray_from_c(sq, dx[row], dy[row]);
-            t.r[row * 64 + sq] = row < 3 ? r : rev64_c(r);
-        }
-    return t;
-}
-__constant__ RayTable kRayTable = make_ray_table();
 
 // flips of the move on empty square sq (Board.put's count is their popcount,
 // board.py:161-174); 0 when nothing is flanked.  Horizontal runs by the carry
 // on the inner files (no ray mask needed), the six others by ray_flips; rays
-// leaving in decreasing bit order on the bit-reversed board (tab rows 3..5).
-__device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O, const u64* tab) {
+// leaving in decreasing bit order on the bit-reversed board.
+__device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
+    u64 R[kRayRows];
+    rays_of(sq, R);
     const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
     const u64 rP = rev64(P), rO = rev64(O);
     const u64 Oi = O & INNER_FILES, rOi = rO & INNER_FILES;
     const u64 se = Oi + (mv << 1), sw = rOi + (rmv << 1);
     u64 f = (se & P) ? andn(Oi, se) : 0ull;
     u64 fr = (sw & rP) ? andn(rOi, sw) : 0ull;
-    f = or3(f, ray_flips(mv << 8, tab[0 * 64 + sq], P, O), ray_flips(mv << 9, tab[1 * 64 + sq], P, O));
-    f |= ray_flips(mv << 7, tab[2 * 64 + sq], P, O);
-    fr = or3(fr, ray_flips(rmv << 8, tab[3 * 64 + sq], rP, rO), ray_flips(rmv << 9, tab[4 * 64 + sq], rP, rO));
-    fr |= ray_flips(rmv << 7, tab[5 * 64 + sq], rP, rO);
+    f = or3(f, ray_flips(mv << 8, R[0], P, O), ray_flips(mv << 9, R[1], P, O));
+    f |= ray_flips(mv << 7, R[2], P, O);
+    fr = or3(fr, ray_flips(rmv << 8, R[3], rP, rO), ray_flips(rmv << 9, R[4], rP, rO));
+    fr |= ray_flips(rmv << 7, R[5], rP, rO);
     return f | rev64(fr);
 }
 
@@ -266,27 +261,6 @@ __device__ __forceinline__ u64 moves_empty_side(u64 black, u64 white) {
     Position s;
     analyse(E, black, s);
     return s.reach & E;
-}
-
-// flips of `mv` for mover P with a bracket test per direction (used where the run
-// sets of the position are not available: the single-step kernel).  Works for any
-// mv; returns 0 when nothing is flanked.
-// (no wrap mask on the bracket test: a run is confined to the propagator's inner
-// files, so only the run-less case g == mv can "wrap", and it flips nothing)
-template <int S, bool L>
-__device__ __forceinline__ u64 flips_dir_test(u64 mv, u64 P, const PairProp& q) {
-    const u64 g = ks<S, L>(mv, q);
-    return (sh<S, L>(g) & P) ? g : 0ull;
-}
-__device__ __forceinline__ u64 flips_tested(u64 mv, u64 P, u64 O) {
-    const u64 Oi = O & INNER_FILES;
-    const PairProp h = pair_prop<1>(Oi), v = pair_prop<8>(O), d9 = pair_prop<9>(Oi), d7 = pair_prop<7>(Oi);
-    const u64 e = east_run(mv, Oi);  // run east of mv; flanked iff the square after it is P
-    u64 f = ((((e | mv) << 1) & P) ? e : 0ull) | flips_dir_test<1, false>(mv, P, h);
-    f |= flips_dir_test<8, true>(mv, P, v) | flips_dir_test<8, false>(mv, P, v);
-    f |= flips_dir_test<9, true>(mv, P, d9) | flips_dir_test<9, false>(mv, P, d9);
-    f |= flips_dir_test<7, true>(mv, P, d7) | flips_dir_test<7, false>(mv, P, d7);
-    return andn(f, mv);
 }
 
 // k-th set bit via two popcount bisection levels (32, 16, 8) and a 256x8 byte

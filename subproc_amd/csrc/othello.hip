@@ -2,7 +2,7 @@
 //
 // Replaces the step path of ysnrkdm/subproc board.py:
 //   puttables / n_puttable_for  (board.py:46-55)   -> moves(): Kogge-Stone fills + carry rays
-//   put / put_s                 (board.py:161-209) -> step: flips_tested; rollouts: flips_rays
+//   put / put_s                 (board.py:161-209) -> step: flips_carry; rollouts: flips_rays
 //                                                     (LDS ray table + run-set prefix)
 //   is_game_over                (board.py:57-58)   -> two-pass rule in the rollout loop
 //   n_black / n_white + result  (board.py:37-41, game_runner.py:194-199)
@@ -233,8 +233,8 @@ __global__ __launch_bounds__(kBlock) void legal_kernel(const u64* __restrict__ b
 }
 
 // one board of the step (board.py:192-209 semantics, see include/othello.h)
-__device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 mvc, const u64* rays, u64* boards_out,
-                                           uint8_t* turn_out, u64* __restrict__ flips_out,
+__device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 mvc, u64* boards_out, uint8_t* turn_out,
+                                           u64* __restrict__ flips_out,
                                            u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
                                            uint8_t* __restrict__ nturn) {
     const bool valid_turn = (t == OTH_BLACK) | (t == OTH_WHITE);
@@ -249,7 +249,7 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
         } else if (mvc < 64) {
             const u64 mv = 1ull << mvc;
             if (!((P | O) & mv)) {
-                f = flips_carry(mvc, P, O, rays);
+                f = flips_carry(mvc, P, O);
                 if (f) {
                     r = __popcll(f);
                     P |= f | mv;
@@ -283,26 +283,14 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, cons
                                                       uint8_t* turn_out, u64* __restrict__ flips_out,
                                                       u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
                                                       uint8_t* __restrict__ nturn, int64_t n) {
-    __shared__ u64 rays[kRayRows * 64];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool in = i < n;
-    ulonglong2 b = make_ulonglong2(0, 0);
-    u32 t = 0, mvc = 0;
-    if (in) {
-        b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
-        t = turn_in[i];
-        mvc = move[i];
-    }
-    // the ray table (3 KiB, L2-resident) rides along with the board loads
-    static_assert(kRayRows * 32 <= kBlock, "one 16-byte table piece per thread");
-    if (threadIdx.x < kRayRows * 32)
-        reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = reinterpret_cast<const ulonglong2*>(kRayTable.r)[threadIdx.x];
-    // all loads in flight together: without this hipcc sinks the move load into
-    // the valid-turn branch, a second dependent HBM round trip per wave
+    if (i >= n) return;
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
+    const u32 t = turn_in[i], mvc = move[i];
+    // all three loads in flight together: without this hipcc sinks the move
+    // load into the valid-turn branch, a second dependent HBM round trip per wave
     asm volatile("" ::"v"(t), "v"(mvc));
-    __syncthreads();
-    if (!in) return;
-    step_board(i, b, t, mvc, rays, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
+    step_board(i, b, t, mvc, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
 }
 
 __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ boards, uint8_t* __restrict__ nb,
@@ -581,8 +569,9 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
                 return;
             }
             if (legal) {
-                const u64 mv = 1ull << kth_bit(legal, rng.pick((u32)__popcll(legal)));
-                const u64 f = flips_tested(mv, P, O);
+                const u32 sq = kth_bit(legal, rng.pick((u32)__popcll(legal)));
+                const u64 mv = 1ull << sq;
+                const u64 f = flips_carry(sq, P, O);
                 P |= f | mv;
                 O = andn(O, f);
             }
@@ -649,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ 
                         u64 P = black ? bl : wh, O = black ? wh : bl;
                         const u64 mm = 1ull << c;
                         if (!((P | O) & mm)) {
-                            const u64 f = flips_tested(mm, P, O);
+                            const u64 f = flips_carry(c, P, O);
                             if (f) {
                                 P |= f | mm;
                                 O = andn(O, f);

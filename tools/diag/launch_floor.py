@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from subproc_amd import _lib, ops  # noqa: E402
 
 lib = _lib.load()
-n = 65536
+n = int(os.environ.get("LF_N", 65536))
 pos = ops.sample_midgame(n, 0x5EED, device="cuda")
 bo, to = torch.empty_like(pos.boards), torch.empty_like(pos.turn)
 fl, ln = torch.empty(n, dtype=torch.int64, device="cuda"), torch.empty(n, dtype=torch.int64, device="cuda")

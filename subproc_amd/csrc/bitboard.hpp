@@ -25,19 +25,15 @@ typedef uint32_t u32;
 
 constexpr u64 INNER_FILES = 0x7E7E7E7E7E7E7E7Eull;  // files b..g: a disc on a/h cannot be flanked along a row/diagonal
 
-// bfi(m, a, b) = (m & a) | (~m & b): one v_bfi_b32 per half.  Every Kogge-Stone
+// bfi(m, a, b) = (m & a) | (~m & b): one 3-input op per half.  Every Kogge-Stone
 // step "gen |= pro & shifted" is written as bfi(pro, shifted, gen): the propagator
 // never intersects the current fill (a propagator square at distance <= 2^k from
-// the source would need an opponent disc at distance 0), so both forms agree, and
-// hipcc emits bfi (it never fuses the plain and-or).  Flip accumulation uses the
-// same identity: rays from one square are disjoint.
-__device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return (m & a) | (~m & b); }
-__device__ __forceinline__ u64 andn(u64 a, u64 b) { return a & ~b; }
-__device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return a | b | c; }
-
-// any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the truth
-// table indexed by (a, b, c) bits: 0x80 = a & b & c, 0x20 = a & ~b & c, 0x04 = ~a & b & ~c
-// (each reads the same under either operand order of the index).
+// the source would need an opponent disc at distance 0), so both forms agree
+// (hipcc never fuses the plain and-or).
+// any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the
+// function's value on (a, b, c) = (0xF0, 0xCC, 0xAA): 0xCA = a ? b : c,
+// 0x80 = a & b & c, 0xFE = a | b | c, 0x30 = a & ~b, 0x20 = a & ~b & c,
+// 0x04 = ~a & b & ~c.
 template <int TT>
 __device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
     // (the builtin returns int: take both halves as u32, no sign extension)
@@ -45,9 +41,24 @@ __device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
     const u32 lo = (u32)__builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, TT);
     return ((u64)hi << 32) | lo;
 }
+// The three-input logic of these kernels goes through v_bitop3_b32 by hand:
+// measured on the box (tools/diag/valu_rate4.cpp, 8 waves/SIMD) it issues in
+// 2.4-3.4 cycles per wave-instruction where v_bfi_b32 and v_or3_b32 take 4.2,
+// and hipcc emits bfi / or3 / bfi-with-0 for these forms on its own.
+__device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return bitop3<0xCA>(m, a, b); }
+__device__ __forceinline__ u64 andn(u64 a, u64 b) { return bitop3<0x30>(a, b, b); }
+__device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return bitop3<0xFE>(a, b, c); }
+// 64-bit shifts as single v_lshlrev_b64 / v_lshrrev_b64 (inline asm): with
+// the 3-input logic taken apart into 32-bit halves, hipcc's combiner would
+// otherwise split each shift into v_lshlrev_b32 + v_alignbit_b32, two
+// instructions where one 64-bit shift issues as fast (valu_rate4.cpp).
 template <int S, bool L>
 __device__ __forceinline__ u64 sh(u64 x) {
-    return L ? (x << S) : (x >> S);
+    static_assert(S > 0 && S < 64, "shift amount");
+    u64 r;
+    if (L) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(S));
+    else asm("v_lshrrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(S));
+    return r;
 }
 
 // Kogge-Stone propagators of one direction pair (+S / -S) for opponent set `pro`
@@ -79,7 +90,24 @@ __device__ __forceinline__ u64 ks(u64 gen, const PairProp& q) {
 // `src`: the carry of Oi + (src << 1) ripples through each such run (one
 // v_lshl_add_u64 + one v_bfi_b32 per half); equal to the Kogge-Stone east fill
 // from src through Oi, minus src.
-__device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, (src << 1) + Oi); }
+// 64-bit adds as one v_lshl_add_u64 each (inline asm, for the same reason as
+// sh: an add of a value assembled from halves is otherwise split in two)
+__device__ __forceinline__ u64 lshl1_add(u64 x, u64 y) {  // (x << 1) + y
+    u64 r;
+    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ u64 add64(u64 x, u64 y) {
+    u64 r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ u64 dec64(u64 x) {  // x - 1
+    u64 r;
+    asm("v_lshl_add_u64 %0, %1, 0, -1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, lshl1_add(src, Oi)); }
 
 // 64-bit bit reversal (two v_bfrev_b32, halves swapped): square sq <-> 63 - sq,
 // which turns the west ray into an east ray.
@@ -158,7 +186,7 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
 __device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bitop3<0x80>(a, b, c); }
 __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
     const u64 x = andn(R, A);
-    return and3(R, A, x - 1);
+    return and3(R, A, dec64(x));
 }
 
 // The run sets flips_rays reads, in the orientation it reads them: the runs
@@ -200,7 +228,7 @@ __device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, cons
 // of the ray: no stop square, no flips.  An off-board ray is empty, so nothing
 // is selected from it.
 __device__ __forceinline__ u64 ray_flips(u64 first, u64 R, u64 P, u64 O) {
-    const u64 sum = bfi(R, O, ~0ull) + first;   // (O | ~R) + first
+    const u64 sum = add64(bfi(R, O, ~0ull), first);  // (O | ~R) + first
     const u64 run = bitop3<0x20>(R, sum, O);    // R & ~sum & O
     return and3(sum, R, P) ? run : 0ull;        // stop square is P
 }
@@ -235,7 +263,7 @@ __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
     const u64 rP = rev64(P), rO = rev64(O);
     const u64 Oi = O & INNER_FILES, rOi = rO & INNER_FILES;
-    const u64 se = Oi + (mv << 1), sw = rOi + (rmv << 1);
+    const u64 se = lshl1_add(mv, Oi), sw = lshl1_add(rmv, rOi);
     u64 f = (se & P) ? andn(Oi, se) : 0ull;
     u64 fr = (sw & rP) ? andn(rOi, sw) : 0ull;
     f = or3(f, ray_flips(mv << 8, R[0], P, O), ray_flips(mv << 9, R[1], P, O));

@@ -105,7 +105,7 @@ template <int POLICY>
 __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab) {
     const u64 mv = 1ull << sq;
     const u64 f = flips_rays(sq, mv, s, rays);
-    const u64 P2 = P | f | mv, O2 = andn(O, f);
+    const u64 P2 = or3(P, f, mv), O2 = andn(O, f);
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
     // every child has popcount(P|O) + 1 discs: one weight row per parent
     const int* row = w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
@@ -252,7 +252,7 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
                 f = flips_carry(mvc, P, O);
                 if (f) {
                     r = __popcll(f);
-                    P |= f | mv;
+                    P = or3(P, f, mv);
                     O = andn(O, f);
                 }
             }
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                     const u64 np = andn(O, f);
-                    O = P | f | mv;
+                    O = or3(P, f, mv);
                     P = np;
                     ply++;
                 }
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                     const u64 np = andn(O, f);
-                    O = P | f | mv;
+                    O = or3(P, f, mv);
                     P = np;
                     side ^= 3u;
                     ply++;
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
                 const u32 sq = kth_bit(legal, rng.pick((u32)__popcll(legal)));
                 const u64 mv = 1ull << sq;
                 const u64 f = flips_carry(sq, P, O);
-                P |= f | mv;
+                P = or3(P, f, mv);
                 O = andn(O, f);
             }
             const u64 t = P;

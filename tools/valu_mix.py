@@ -5,9 +5,10 @@ bench.py prices the integer kernels against (profiles/valu_mix.json).
 CDNA4 SIMDs are 32 lanes wide: a wave64 VALU instruction can issue every 2
 cycles (MI355X_MICROARCH.md, cycle constants).  Measured on the box
 (tools/diag/valu_rate*.cpp, DESIGN.md §3 cost model), only plain VOP2 logic
-(v_and/or/xor/not/mov) streams at ~2.2 cycles; 64-bit shifts, v_bfi_b32,
-v_or3/bitop3, v_bcnt, v_cndmask, 32-bit shifts and SGPR-operand forms take ~4.
-So a kernel's ceiling is 1024 SIMDs x clock / (mean cycles over its mix).
+(v_and/or/xor/not/mov) streams at ~2.2 cycles, v_bitop3_b32 at ~3.35;
+64-bit shifts, v_bfi_b32, v_or3_b32, v_bcnt, v_cndmask, 32-bit shifts and
+SGPR-operand forms take ~4 (table MEASURED).  So a kernel's ceiling is 1024
+SIMDs x clock / (mean cycles over its mix).
 Unmeasured VOP2 forms (add/sub/min/max) are counted as fast, which raises the
 ceiling (the conservative side for a fraction-of-peak claim).
 
@@ -28,6 +29,18 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAST = re.compile(r"^v_(and|or|xor|not|mov|add|sub|subrev|min|max)_(b32|u32|i32|b64)_e32$")
 FAST_CYC, SLOW_CYC = 2.2, 4.0
+# measured issue cost of the instructions these kernels are made of (cycles per
+# wave-instruction per SIMD, 8 waves/SIMD, tools/diag/valu_rate4.cpp on the box);
+# anything else not FAST is SLOW_CYC
+MEASURED = {"v_bitop3_b32": 3.35, "v_bfi_b32": 4.2, "v_or3_b32": 4.2, "v_lshlrev_b64": 4.1, "v_lshrrev_b64": 4.15,
+            "v_lshl_add_u64": 4.65, "v_bfrev_b32_e32": 4.05, "v_alignbit_b32": 4.2, "v_perm_b32": 4.3,
+            "v_lshlrev_b32_e32": 4.0}
+
+
+def cycles(op):
+    if op in MEASURED:
+        return MEASURED[op]
+    return FAST_CYC if FAST.match(op) else SLOW_CYC
 KERNELS = {"rollout_kernel<0, false>": "rollout_kernelILi0ELb0E", "rollout_kernel<1, false>": "rollout_kernelILi1ELb0E",
            "rollout_kernel<2, false>": "rollout_kernelILi2ELb0E", "step_kernel": "step_kernel"}
 
@@ -86,7 +99,7 @@ def hot_loop_mix(body):
     h, ops = max(inner.items(), key=lambda kv: len(kv[1]))
     fast = sum(1 for o in ops if FAST.match(o))
     slow = len(ops) - fast
-    mean = (fast * FAST_CYC + slow * SLOW_CYC) / max(1, len(ops))
+    mean = sum(cycles(o) for o in ops) / max(1, len(ops))
     return {"loop_header": h, "valu": len(ops), "fast_vop2": fast, "slow": slow, "mean_cycles": round(mean, 3),
             "top": collections.Counter(ops).most_common(8)}
 
@@ -106,7 +119,7 @@ def main():
                     ops = [m.group(1) for m in (re.match(r"^\s+(v_[a-z0-9_]+)", ln) for ln in body) if m]
                     fast = sum(1 for o in ops if FAST.match(o))
                     r = {"loop_header": None, "valu": len(ops), "fast_vop2": fast, "slow": len(ops) - fast,
-                         "mean_cycles": round((fast * FAST_CYC + (len(ops) - fast) * SLOW_CYC) / max(1, len(ops)), 3),
+                         "mean_cycles": round(sum(cycles(o) for o in ops) / max(1, len(ops)), 3),
                          "top": collections.Counter(ops).most_common(8)}
                 r["peak_winstr_s"] = out["simds"] * out["clock_ghz"] * 1e9 / r["mean_cycles"]
                 out["kernels"][k] = r

@@ -209,7 +209,7 @@ __device__ __forceinline__ RunSets run_sets(const Position& s) {
 // The other six by the ray tables (run_prefix).
 __device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, const u64* tab) {
     u64 f = east_run(mv, r.A1);
-    u64 fr = east_run(rev64(mv), r.rA0);  // west, in reversed space
+    u64 fr = east_run(1ull << (sq ^ 63u), r.rA0);  // west, in reversed space (rev64(mv))
     f = or3(f, run_prefix(tab[0 * 64 + sq], r.A3), run_prefix(tab[1 * 64 + sq], r.A5));
     f |= run_prefix(tab[2 * 64 + sq], r.A7);
     fr = or3(fr, run_prefix(tab[3 * 64 + sq], r.rA2), run_prefix(tab[4 * 64 + sq], r.rA4));

@@ -26,6 +26,10 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed) {
         if (OP == 12) asm volatile(B8("v_bitop3_b32 %0, %4, %1, %0 bitop3:0xca\n v_bitop3_b32 %1, %4, %2, %1 bitop3:0xca\n v_bitop3_b32 %2, %4, %3, %2 bitop3:0xca\n v_bitop3_b32 %3, %4, %0, %3 bitop3:0xca") : "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(m));
         if (OP == 13) asm volatile(B8("v_bfi_b32 %0, %1, %2, %0\n v_bfi_b32 %1, %2, %3, %1\n v_bfi_b32 %2, %3, %0, %2\n v_bfi_b32 %3, %0, %1, %3") : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
         if (OP == 14) asm volatile(B8("v_or3_b32 %0, %1, %2, %0\n v_or3_b32 %1, %2, %3, %1\n v_or3_b32 %2, %3, %0, %2\n v_or3_b32 %3, %0, %1, %3") : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
+        if (OP == 16) asm volatile(B8("v_add_co_u32_e32 %0, vcc, %2, %0\n v_addc_co_u32_e32 %1, vcc, %3, %1, vcc\n v_add_co_u32_e32 %2, vcc, %0, %2\n v_addc_co_u32_e32 %3, vcc, %1, %3, vcc") : "+v"(x), "+v"(y), "+v"(z), "+v"(w) :: "vcc");
+        if (OP == 17) asm volatile(B8("v_bcnt_u32_b32 %0, %1, 0\n v_bcnt_u32_b32 %1, %2, 0\n v_bcnt_u32_b32 %2, %3, 0\n v_bcnt_u32_b32 %3, %0, 0") : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
+        if (OP == 18) asm volatile(B8("v_cndmask_b32_e32 %0, %1, %0, vcc\n v_cndmask_b32_e32 %1, %2, %1, vcc\n v_cndmask_b32_e32 %2, %3, %2, vcc\n v_cndmask_b32_e32 %3, %0, %3, vcc") : "+v"(x), "+v"(y), "+v"(z), "+v"(w) :: "vcc");
+        if (OP == 19) asm volatile(B8("v_and_or_b32 %0, %1, %2, %0\n v_and_or_b32 %1, %2, %3, %1\n v_and_or_b32 %2, %3, %0, %2\n v_and_or_b32 %3, %0, %1, %3") : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
         if (OP == 15) asm volatile(B8("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xca\n v_bitop3_b32 %1, %2, %3, %1 bitop3:0xca\n v_bitop3_b32 %2, %3, %0, %2 bitop3:0xca\n v_bitop3_b32 %3, %0, %1, %3 bitop3:0xca") : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
     }
     out[blockIdx.x * 256 + threadIdx.x] = x ^ y ^ z ^ w ^ (unsigned)a ^ (unsigned)b ^ (unsigned)c ^ (unsigned)d;
@@ -51,16 +55,18 @@ int main() {
     const char* names[] = {"lshlrev_b64 imm", "lshrrev_b64 imm", "lshl_add_u64", "alignbit_b32", "perm_b32",
                            "lshlrev_b32", "bfi_b32", "and_b32", "lshlrev_b64 vgpr amt", "1 shl_b64 + 3 bfi",
                            "bitop3_b32 (and3)", "bfrev_b32", "bitop3 0xca, bfi's operands", "bfi, bitop3's operands",
-                           "or3_b32", "bitop3 0xca, own operands"};
+                           "or3_b32", "bitop3 0xca, own operands", "add_co/addc_co e32 (2/64-bit add)",
+                           "bcnt_u32", "cndmask_e32 vcc", "and_or_b32"};
     for (int i = 0; i < 3; i++) run<0>(out, 2048);  // clock ramp
-    for (int blocks : {1024, 2048}) {
+    for (int blocks : {2048}) {
         printf("-- %d waves/SIMD\n", blocks / 256);
-        float t[16];
+        float t[20];
         t[0] = run<0>(out, blocks); t[1] = run<1>(out, blocks); t[2] = run<2>(out, blocks); t[3] = run<3>(out, blocks);
         t[4] = run<4>(out, blocks); t[5] = run<5>(out, blocks); t[6] = run<6>(out, blocks); t[7] = run<7>(out, blocks);
         t[8] = run<8>(out, blocks); t[9] = run<9>(out, blocks); t[10] = run<10>(out, blocks); t[11] = run<11>(out, blocks);
         t[12] = run<12>(out, blocks); t[13] = run<13>(out, blocks); t[14] = run<14>(out, blocks); t[15] = run<15>(out, blocks);
-        for (int op = 0; op < 16; op++) {
+        t[16] = run<16>(out, blocks); t[17] = run<17>(out, blocks); t[18] = run<18>(out, blocks); t[19] = run<19>(out, blocks);
+        for (int op = 0; op < 20; op++) {
             const double winstr = (double)blocks * 4 * ITERS * 32;
             printf("  %-24s %.3f ms  %.2f cyc/instr/SIMD @2.4GHz\n", names[op], t[op],
                    1024 * 2.4e9 / (winstr / (t[op] * 1e-3)));

@@ -1,11 +1,13 @@
 // bitboard.hpp — gfx950 device primitives for 8x8 Othello bitboards.
 //
 // Cost model (measured on MI355X, tools/diag/valu_rate*.cpp, DESIGN.md §Cost model):
-// in a mixed VALU stream every VALU instruction costs ~4 cycles per wave64 on its
-// SIMD (only pure streams of simple VOP2 logic reach ~2.2), so throughput is set by
-// the INSTRUCTION COUNT per env-step.  Hence:
-//   * 64-bit shifts stay single v_lshl/v_lshrrev_b64 instructions;
-//   * every fill step / flip accumulation is one v_bfi_b32 per 32-bit half (see bfi);
+// a kernel's throughput is the issue cost of its VALU instructions per env-step.
+// Plain VOP2 logic issues in ~2.2 cycles per wave64, v_bitop3_b32 in ~3.35, and
+// nearly everything else (64-bit shifts, v_bfi/v_or3, v_bcnt, v_cndmask,
+// v_bfrev) in ~4-4.6.  Hence:
+//   * 64-bit shifts and adds stay single v_lshl/v_lshrrev_b64 / v_lshl_add_u64;
+//   * all 3-input logic (fill steps, masks, flip accumulation) is one
+//     v_bitop3_b32 per 32-bit half (bitop3, bfi, andn, or3);
 //   * Kogge-Stone propagators are computed once per position and shared between
 //     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S);
 //   * the chosen move's flips come from per-square ray tables in LDS and the
@@ -25,11 +27,6 @@ typedef uint32_t u32;
 
 constexpr u64 INNER_FILES = 0x7E7E7E7E7E7E7E7Eull;  // files b..g: a disc on a/h cannot be flanked along a row/diagonal
 
-// bfi(m, a, b) = (m & a) | (~m & b): one 3-input op per half.  Every Kogge-Stone
-// step "gen |= pro & shifted" is written as bfi(pro, shifted, gen): the propagator
-// never intersects the current fill (a propagator square at distance <= 2^k from
-// the source would need an opponent disc at distance 0), so both forms agree
-// (hipcc never fuses the plain and-or).
 // any 3-input bitwise function as one v_bitop3_b32 per half.  TT is the
 // function's value on (a, b, c) = (0xF0, 0xCC, 0xAA): 0xCA = a ? b : c,
 // 0x80 = a & b & c, 0xFE = a | b | c, 0x30 = a & ~b, 0x20 = a & ~b & c,
@@ -45,6 +42,10 @@ __device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
 // measured on the box (tools/diag/valu_rate4.cpp, 8 waves/SIMD) it issues in
 // 2.4-3.4 cycles per wave-instruction where v_bfi_b32 and v_or3_b32 take 4.2,
 // and hipcc emits bfi / or3 / bfi-with-0 for these forms on its own.
+// bfi(m, a, b) = (m & a) | (~m & b).  Every Kogge-Stone step "gen |= pro &
+// shifted" is written as bfi(pro, shifted, gen): the propagator never
+// intersects the current fill (a propagator square at distance <= 2^k from the
+// source would need an opponent disc at distance 0), so both forms agree.
 __device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return bitop3<0xCA>(m, a, b); }
 __device__ __forceinline__ u64 andn(u64 a, u64 b) { return bitop3<0x30>(a, b, b); }
 __device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return bitop3<0xFE>(a, b, c); }
@@ -86,10 +87,6 @@ __device__ __forceinline__ u64 ks(u64 gen, const PairProp& q) {
     return gen;
 }
 
-// discs of `Oi` (inner opponent discs) in runs that start right east of a bit of
-// `src`: the carry of Oi + (src << 1) ripples through each such run (one
-// v_lshl_add_u64 + one v_bfi_b32 per half); equal to the Kogge-Stone east fill
-// from src through Oi, minus src.
 // 64-bit adds as one v_lshl_add_u64 each (inline asm, for the same reason as
 // sh: an add of a value assembled from halves is otherwise split in two)
 __device__ __forceinline__ u64 lshl1_add(u64 x, u64 y) {  // (x << 1) + y
@@ -107,6 +104,10 @@ __device__ __forceinline__ u64 dec64(u64 x) {  // x - 1
     asm("v_lshl_add_u64 %0, %1, 0, -1" : "=v"(r) : "v"(x));
     return r;
 }
+// discs of `Oi` (inner opponent discs) in runs that start right east of a bit of
+// `src`: the carry of Oi + (src << 1) ripples through each such run (one
+// v_lshl_add_u64 + one v_bitop3_b32 per half); equal to the Kogge-Stone east
+// fill from src through Oi, minus src.
 __device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, lshl1_add(src, Oi)); }
 
 // 64-bit bit reversal (two v_bfrev_b32, halves swapped): square sq <-> 63 - sq,

@@ -188,6 +188,16 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
 int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,
                double* out, int64_t n_seg, void* stream);
 
+/* oth_td_ema with the long segments split off: segments of length >= long_min
+ * are each run by a whole wavefront (the wave stages the segment's values
+ * through LDS, one lane runs the chain), the others one per thread as in
+ * oth_td_ema.  long_idx (device, n_long entries) must list every segment of
+ * length >= long_min, in any order, each once; a segment that long missing
+ * from it is left unwritten.  Same results as oth_td_ema, bit for bit. */
+int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
+                     double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
+                     int64_t n_long, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

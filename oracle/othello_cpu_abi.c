@@ -181,6 +181,14 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
     return OTH_OK;
 }
 
+int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
+                     double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
+                     int64_t n_long, void* stream) {
+    /* the split only changes how the GPU schedules segments: every segment in order here */
+    if (long_min < 1 || n_long < 0 || (n_long > 0 && !long_idx)) return OTH_EINVAL;
+    return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
+}
+
 int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
              void* stream) {
     (void)stream;

@@ -832,15 +832,17 @@ __device__ __forceinline__ double td_run_full(double v, const double (&b)[kTdChu
     }
     return zero ? td_run(v, b, kTdChunk, a, oma) : w;
 }
+// long_min: segments at least this long belong to td_ema_long_kernel (0: none)
 __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
                                                         const int64_t* __restrict__ seg_off,
                                                         const double* __restrict__ init, double a, double oma,
-                                                        double* __restrict__ out, int64_t n_seg) {
+                                                        double* __restrict__ out, int64_t n_seg, int64_t long_min) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= n_seg) return;
-    double v = init ? init[s] : 0.0;
     int64_t i = seg_off[s];
     const int64_t e = seg_off[s + 1];
+    if (long_min > 0 && e - i >= long_min) return;
+    double v = init ? init[s] : 0.0;
     if (e - i < 3 * kTdChunk) {  // the common case: a handful of updates
         for (; i < e; i++) v = td_step(v, vals[i], a, oma);
         out[s] = v;
@@ -864,6 +866,85 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
     v = td_run(v, b1, r - kTdChunk, a, oma);
     v = td_run(v, b2, r - 2 * kTdChunk, a, oma);
     out[s] = v;
+}
+
+// One long segment per single-wave block.  A thread alone is bound by how many
+// loads it keeps in flight (~30 dwordx2: the 524,288-update opening key of a
+// 262,144-game batch took ~13 ms); here the whole wave stages the segment
+// through LDS with coalesced loads, double-buffered, and lane 0 runs the chain
+// from LDS while the next stage is in flight, so the time is the chain's.
+constexpr int kTdStage = 1024;                 // doubles per LDS stage
+constexpr int kTdStageLoads = kTdStage / 64;   // loads per lane per stage
+__global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ vals,
+                                                         const int64_t* __restrict__ seg_off,
+                                                         const double* __restrict__ init, double a, double oma,
+                                                         double* __restrict__ out,
+                                                         const int64_t* __restrict__ long_idx) {
+    __shared__ double stage[2][kTdStage], ystage[2][kTdStage];
+    const int lane = threadIdx.x;
+    const int64_t s = long_idx[blockIdx.x];
+    const int64_t b = seg_off[s], e = seg_off[s + 1];
+    const int64_t n_stage = (e - b + kTdStage - 1) / kTdStage;
+    double r[kTdStageLoads];
+    auto fetch = [&](int64_t c) {
+#pragma unroll
+        for (int k = 0; k < kTdStageLoads; k++) {
+            const int64_t idx = b + c * kTdStage + k * 64 + lane;
+            r[k] = idx < e ? vals[idx] : 0.0;
+        }
+    };
+    auto park = [&](int buf) {
+#pragma clang fp contract(off)
+#pragma unroll
+        for (int k = 0; k < kTdStageLoads; k++) {
+            stage[buf][k * 64 + lane] = r[k];
+            ystage[buf][k * 64 + lane] = r[k] * a;  // the chain's x * a, off its critical path
+        }
+    };
+    fetch(0);
+    park(0);
+    __syncthreads();
+    double v = (lane == 0 && init) ? init[s] : 0.0;
+    for (int64_t c = 0; c < n_stage; c++) {
+        if (c + 1 < n_stage) fetch(c + 1);  // in flight while lane 0 runs stage c
+        if (lane == 0) {
+            // the chain; y = x * a was computed by the staging lanes
+            const double* x = stage[c & 1];
+            const double* y = ystage[c & 1];
+            const int m = (int)min<int64_t>(kTdStage, e - b - c * kTdStage);
+            int j = 0;
+            for (; j + kTdChunk <= m; j += kTdChunk) {
+                // One lane issues this chain alone, so every instruction on it
+                // costs its full issue time: the states are tested for an
+                // exact 0 by one multiply per step into a running product
+                // (0 if any state was +-0; an underflow to 0 only sends the
+                // chunk down the exact path, which is always correct) instead
+                // of a compare per step, which doubled the chain's time.
+                double w = v, prod = 1.0;
+#pragma unroll
+                for (int k = 0; k < kTdChunk; k++) {
+#pragma clang fp contract(off)
+                    prod *= w;
+                    w = w * oma + y[j + k];
+                }
+                const bool zero = prod == 0.0;
+                if (zero) {  // a state was exactly 0: redo the chunk with the exact rule
+                    double bk[kTdChunk];
+#pragma unroll
+                    for (int k = 0; k < kTdChunk; k++) bk[k] = x[j + k];
+                    w = td_run(v, bk, kTdChunk, a, oma);
+                }
+                v = w;
+            }
+            double bk[kTdChunk];
+#pragma unroll
+            for (int k = 0; k < kTdChunk; k++) bk[k] = x[min(j + k, kTdStage - 1)];
+            v = td_run(v, bk, m - j, a, oma);
+        }
+        if (c + 1 < n_stage) park((c + 1) & 1);
+        __syncthreads();
+    }
+    if (lane == 0) out[s] = v;
 }
 
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
@@ -1117,7 +1198,23 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
     if (n_seg < 0 || (n_seg > 0 && (!values || !seg_off || !out))) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
     td_ema_kernel<<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a, out,
-                                                                         n_seg);
+                                                                         n_seg, 0);
+    return launched();
+}
+
+int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
+                     double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
+                     int64_t n_long, void* stream) {
+    if (n_seg < 0 || long_min < 1 || n_long < 0 || n_long > n_seg ||
+        (n_seg > 0 && (!values || !seg_off || !out)) || (n_long > 0 && !long_idx))
+        return OTH_EINVAL;
+    if (n_seg == 0) return OTH_OK;
+    td_ema_kernel<<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a, out,
+                                                                         n_seg, long_min);
+    int rc = launched();
+    if (rc != OTH_OK || n_long == 0) return rc;
+    td_ema_long_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
+                                                                         out, long_idx);
     return launched();
 }
 

@@ -15,9 +15,10 @@ Here the whole batch runs on the device:
   1. ``oth_td_updates`` (HIP) emits the ordered update stream: packed counts()
      key + value per (position, side), from an ``oth_replay`` position table;
   2. a stable sort by key (torch) groups each key's updates in stream order;
-  3. ``oth_td_ema`` (HIP) replays each key's updates sequentially in float64
-     with separate multiply and add, so every value is bit-identical to the
-     Python learner's;
+  3. ``oth_td_ema_split`` (HIP) replays each key's updates sequentially in
+     float64 with separate multiply and add, so every value is bit-identical
+     to the Python learner's (a key with at least LONG_MIN updates gets a
+     whole wavefront, which stages its values through LDS);
   4. the result is merged into the device-resident, key-sorted table.
 Batches applied one after another equal one batch of all their books.
 Values are kept as float64 (the Python learner's float, before any store
@@ -35,6 +36,7 @@ from .params import SHARDS
 
 A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
 LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
+LONG_MIN = 1024  # updates per key from which oth_td_ema_split runs the key on a whole wave
 _SHIFTS = (47, 40, 35, 30, 25, 20, 15, 10, 5, 0)
 _WIDTH = (7, 7, 5, 5, 5, 5, 5, 5, 5, 5)
 
@@ -121,8 +123,12 @@ class StateMap:
                 cl = pos_in_old.clamp(max=len(self) - 1)
                 init = torch.where(self.keys[cl] == ukeys, self.values[cl], init)
             out = torch.empty_like(init)
-            check(lib.oth_td_ema(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
-                                 out.data_ptr(), ukeys.numel(), stream), "oth_td_ema")
+            # keys with many updates (the opening and the first plies of every
+            # game) are each run by a whole wavefront (oth_td_ema_split)
+            long_idx = torch.nonzero(counts >= LONG_MIN).flatten()
+            check(lib.oth_td_ema_split(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
+                                       out.data_ptr(), ukeys.numel(), LONG_MIN, long_idx.data_ptr(),
+                                       long_idx.numel(), stream), "oth_td_ema_split")
             if pos_in_old is None:
                 self.keys, self.values = ukeys, out
             else:

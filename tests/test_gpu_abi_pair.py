@@ -139,6 +139,13 @@ def test_td_pair():
     out = Buf(np.zeros(len(uk), np.float64))
     both("oth_td_ema", sv, seg, init, 0.03, 1 - 0.03, out, len(uk))
     same(out)
+    lens = np.diff(seg.h)
+    li = Buf(np.flatnonzero(lens >= 48).astype(np.int64))
+    assert 0 < len(li.h) < len(uk)
+    out2 = Buf(np.zeros(len(uk), np.float64))
+    both("oth_td_ema_split", sv, seg, init, 0.03, 1 - 0.03, out2, len(uk), 48, li, len(li.h))
+    same(out2)
+    np.testing.assert_array_equal(out2.h, out.h)
 
 
 def test_empty_null_and_invalid_arguments():
@@ -161,6 +168,7 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_eval(None, None, w, None, 0, s) == 0
         assert lib.oth_td_updates(None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 0, s) == 0
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 1, None, 0, s) == 0
         assert lib.oth_sample_midgame(1, 0, None, None, None, None, 0, s) == 0
         E = _lib.OTH_EINVAL
         assert lib.oth_step(None, None, None, None, None, None, None, None, None, 5, s) == E
@@ -170,6 +178,7 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_rollout_match(None, None, 1, 0, 0, w, None, None, None, None, None, None, 5, s) == E
         assert lib.oth_eval(None, None, None, None, 0, s) == E
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 3, s) == E
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 0, None, 0, s) == E  # long_min < 1
     # every rollout output may be NULL: only the histogram is produced
     n = 4096
     hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))

@@ -48,15 +48,18 @@ def test_state_map_at_scale_vs_oracle():
     assert torch.all(sm.keys[1:] > sm.keys[:-1])  # table stays sorted and unique
 
 
-def test_td_ema_zero_states_in_long_segments():
+@pytest.mark.parametrize("long_min", [None, 48, 1024])
+def test_td_ema_zero_states_in_long_segments(long_min):
     """oth_td_ema speculates that no state in a 16-update chunk is exactly 0 and
     redoes the chunk otherwise: plant exact zero states (a = 0.5, x = -v) at
     chunk starts, middles and ends of long segments and compare with the
-    sequential rule in Python floats."""
+    sequential rule in Python floats.  With long_min, oth_td_ema_split runs
+    the segments at least that long on a whole wave each (LDS stages of 1024
+    values: lengths around multiples of the stage)."""
     from subproc_amd import _lib
     a, oma = 0.5, 0.5
     rng = np.random.default_rng(11)
-    lengths = [1, 5, 47, 48, 49, 63, 64, 100, 1000, 4099]
+    lengths = [1, 5, 47, 48, 49, 63, 64, 100, 1000, 1023, 1024, 1025, 2048, 4099, 12345]
     vals, seg, want = [], [0], []
     for L in lengths:
         v = 0.0 if L % 2 else 0.25
@@ -75,8 +78,14 @@ def test_td_ema_zero_states_in_long_segments():
     ds = torch.tensor(seg, dtype=torch.int64, device=DEV)
     out = torch.empty(len(lengths), dtype=torch.float64, device=DEV)
     lib = _lib.load()
-    _lib.check(lib.oth_td_ema(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(), len(lengths),
-                              torch.cuda.current_stream().cuda_stream), "oth_td_ema")
+    st = torch.cuda.current_stream().cuda_stream
+    if long_min is None:
+        _lib.check(lib.oth_td_ema(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
+                                  len(lengths), st), "oth_td_ema")
+    else:
+        li = torch.tensor([i for i, L in enumerate(lengths) if L >= long_min][::-1], dtype=torch.int64, device=DEV)
+        _lib.check(lib.oth_td_ema_split(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
+                                        len(lengths), long_min, li.data_ptr(), li.numel(), st), "oth_td_ema_split")
     assert out.cpu().tolist() == [w[1] for w in want]
 
 

@@ -62,6 +62,14 @@ out = torch.empty_like(init)
 _lib.check(lib.oth_td_ema(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), 0.03, 0.97, out.data_ptr(),
                           ukeys.numel(), st), "e")
 t = mark("td_ema", t)
+long_idx = torch.nonzero(counts >= td.LONG_MIN).flatten()
+t = mark("long_idx", t)
+out2 = torch.empty_like(init)
+_lib.check(lib.oth_td_ema_split(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), 0.03, 0.97, out2.data_ptr(),
+                                ukeys.numel(), td.LONG_MIN, long_idx.data_ptr(), long_idx.numel(), st), "s")
+t = mark("td_ema_split", t)
+assert torch.equal(out, out2)
+print("long segments", long_idx.numel())
 print("max segment", int(counts.max()), "segments", ukeys.numel(), "updates", total)
 n_old, n_upd = len(sm), ukeys.numel()
 rank_in_upd = torch.searchsorted(ukeys, sm.keys)

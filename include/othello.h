@@ -189,9 +189,11 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
                double* out, int64_t n_seg, void* stream);
 
 /* oth_td_ema with the long segments split off: segments of length >= long_min
- * are each run by a whole wavefront (the wave stages the segment's values
- * through LDS, one lane runs the chain), the others one per thread as in
- * oth_td_ema.  long_idx (device, n_long entries) must list every segment of
+ * are each run by a whole wavefront, the others one per thread as in
+ * oth_td_ema.  Such a wave runs a segment on one lane from LDS stages or, if
+ * the rule contracts (|1 - a| < 1) and the segment is long enough, as up to
+ * 64 parts on its lanes from warm-up guesses of each part's start state, each
+ * guess verified bit for bit and a part rerun when its guess missed.  long_idx (device, n_long entries) must list every segment of
  * length >= long_min, in any order, each once; a segment that long missing
  * from it is left unwritten.  Same results as oth_td_ema, bit for bit. */
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <atomic>
 #include <mutex>
 
@@ -832,21 +833,14 @@ __device__ __forceinline__ double td_run_full(double v, const double (&b)[kTdChu
     }
     return zero ? td_run(v, b, kTdChunk, a, oma) : w;
 }
-// long_min: segments at least this long belong to td_ema_long_kernel (0: none)
-__global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
-                                                        const int64_t* __restrict__ seg_off,
-                                                        const double* __restrict__ init, double a, double oma,
-                                                        double* __restrict__ out, int64_t n_seg, int64_t long_min) {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= n_seg) return;
-    int64_t i = seg_off[s];
-    const int64_t e = seg_off[s + 1];
-    if (long_min > 0 && e - i >= long_min) return;
-    double v = init ? init[s] : 0.0;
+// the rule over vals[i, e) from state v, one thread: short ranges step by
+// step; long ones software-pipelined (a ring of three chunks keeps 2 * kTdChunk
+// loads in flight while the chain consumes the third)
+__device__ double td_range(double v, const double* __restrict__ vals, int64_t i, const int64_t e, double a,
+                           double oma) {
     if (e - i < 3 * kTdChunk) {  // the common case: a handful of updates
         for (; i < e; i++) v = td_step(v, vals[i], a, oma);
-        out[s] = v;
-        return;
+        return v;
     }
     const int64_t last = e - 1;
     double b0[kTdChunk], b1[kTdChunk], b2[kTdChunk];
@@ -865,7 +859,63 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
     v = td_run(v, b0, r, a, oma);
     v = td_run(v, b1, r - kTdChunk, a, oma);
     v = td_run(v, b2, r - 2 * kTdChunk, a, oma);
-    out[s] = v;
+    return v;
+}
+// long_min: segments at least this long belong to td_ema_long_kernel (0: none)
+__global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
+                                                        const int64_t* __restrict__ seg_off,
+                                                        const double* __restrict__ init, double a, double oma,
+                                                        double* __restrict__ out, int64_t n_seg, int64_t long_min) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n_seg) return;
+    const int64_t i = seg_off[s], e = seg_off[s + 1];
+    if (long_min > 0 && e - i >= long_min) return;
+    out[s] = td_range(init ? init[s] : 0.0, vals, i, e, a, oma);
+}
+
+// Speculative split of a very long segment (the opening position's key gets
+// one update per game and side) over the lanes of one wave.  The rule is a
+// contraction (|1 - a| < 1): two runs over the same values from different
+// states approach each other by |1 - a| per step and, once a rounding maps
+// them to the same double, stay equal.  So lane p > 0 guesses the state at
+// the start of its part by a warm-up run over the `warm` values before it,
+// from state 0 (the rule then starts at the first value itself); `warm` is
+// sized by the launcher so that |1 - a|^warm < 2^-64.  Lane p then runs its
+// part from the guess.  Lane 0 checks the guesses in order against the
+// verified end state of the part before, bit for bit: a part whose guess
+// matched has its lane's end state; one whose guess did not is rerun from the
+// verified state.  Every result is thus the sequential one; speculation only
+// decides how fast it comes.
+constexpr int kTdSpecLanes = 64;
+__global__ __launch_bounds__(64) void td_ema_spec_kernel(const double* __restrict__ vals,
+                                                         const int64_t* __restrict__ seg_off,
+                                                         const double* __restrict__ init, double a, double oma,
+                                                         double* __restrict__ out,
+                                                         const int64_t* __restrict__ long_idx, int64_t warm) {
+    __shared__ double guess[kTdSpecLanes], fin[kTdSpecLanes];
+    const int lane = threadIdx.x;
+    const int64_t s = long_idx[blockIdx.x];
+    const int64_t b = seg_off[s], e = seg_off[s + 1];
+    const int64_t n = e - b;
+    if (warm <= 0 || n < 4 * warm) return;  // td_ema_long_kernel's segment
+    const int parts = (int)min<int64_t>(kTdSpecLanes, n / (2 * warm));  // >= 2; every part >= 2 * warm long
+    const int64_t len = (n + parts - 1) / parts;
+    if (lane < parts) {
+        const int64_t i = b + lane * len, j = min(i + len, e);
+        const double g = lane == 0 ? (init ? init[s] : 0.0) : td_range(0.0, vals, i - warm, i, a, oma);
+        guess[lane] = g;
+        fin[lane] = td_range(g, vals, i, j, a, oma);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        double v = fin[0];
+        for (int p = 1; p < parts; p++) {
+            const int64_t i = b + p * len, j = min(i + len, e);
+            if (__double_as_longlong(guess[p]) == __double_as_longlong(v)) v = fin[p];
+            else v = td_range(v, vals, i, j, a, oma);  // the warm-up had not converged: rerun the part
+        }
+        out[s] = v;
+    }
 }
 
 // One long segment per single-wave block.  A thread alone is bound by how many
@@ -879,11 +929,14 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
                                                          const int64_t* __restrict__ seg_off,
                                                          const double* __restrict__ init, double a, double oma,
                                                          double* __restrict__ out,
-                                                         const int64_t* __restrict__ long_idx) {
-    __shared__ double stage[2][kTdStage], ystage[2][kTdStage];
+                                                         const int64_t* __restrict__ long_idx, int64_t warm) {
+    // (ystage rows padded by one chunk: the chain prefetches the next chunk's y
+    // unconditionally)
+    __shared__ double stage[2][kTdStage], ystage[2][kTdStage + kTdChunk];
     const int lane = threadIdx.x;
     const int64_t s = long_idx[blockIdx.x];
     const int64_t b = seg_off[s], e = seg_off[s + 1];
+    if (warm > 0 && e - b >= 4 * warm) return;  // td_ema_spec_kernel's segment
     const int64_t n_stage = (e - b + kTdStage - 1) / kTdStage;
     double r[kTdStageLoads];
     auto fetch = [&](int64_t c) {
@@ -912,29 +965,51 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
             const double* x = stage[c & 1];
             const double* y = ystage[c & 1];
             const int m = (int)min<int64_t>(kTdStage, e - b - c * kTdStage);
-            int j = 0;
-            for (; j + kTdChunk <= m; j += kTdChunk) {
-                // One lane issues this chain alone, so every instruction on it
-                // costs its full issue time: the states are tested for an
-                // exact 0 by one multiply per step into a running product
-                // (0 if any state was +-0; an underflow to 0 only sends the
-                // chunk down the exact path, which is always correct) instead
-                // of a compare per step, which doubled the chain's time.
-                double w = v, prod = 1.0;
+            // One lane issues this chain alone, so every instruction on it
+            // costs its full issue time.  A chunk of kTdChunk steps runs the
+            // two-op rule speculatively and tests its states for an exact 0
+            // by one v_min_f64 of |state| per step (0 iff a state was +-0:
+            // exact, no rounding; a compare per step doubled the chain's
+            // time), then redoes the chunk with the exact rule if one was.
+            // Each step is one asm block so that the min issues between the
+            // chain's multiply and add, in the add's wait.
+            auto chunk = [&](const double(&yk)[kTdChunk], int j0) {
+                double w = v, mn = 1.0;
 #pragma unroll
                 for (int k = 0; k < kTdChunk; k++) {
-#pragma clang fp contract(off)
-                    prod *= w;
-                    w = w * oma + y[j + k];
+                    double t;
+                    asm("v_mul_f64 %[t], %[w], %[oma]\n\t"
+                        "v_min_f64 %[mn], %[mn], |%[w]|\n\t"
+                        "v_add_f64 %[w], %[t], %[y]"
+                        : [w] "+v"(w), [mn] "+v"(mn), [t] "=&v"(t)
+                        : [oma] "v"(oma), [y] "v"(yk[k]));
                 }
-                const bool zero = prod == 0.0;
-                if (zero) {  // a state was exactly 0: redo the chunk with the exact rule
+                if (mn == 0.0) {  // a state was exactly 0: redo the chunk with the exact rule
                     double bk[kTdChunk];
 #pragma unroll
-                    for (int k = 0; k < kTdChunk; k++) bk[k] = x[j + k];
+                    for (int k = 0; k < kTdChunk; k++) bk[k] = x[j0 + k];
                     w = td_run(v, bk, kTdChunk, a, oma);
                 }
                 v = w;
+            };
+            // two chunk buffers: the next chunk's y is read from LDS while a
+            // chunk runs (reads past m stay in the padded row, unused)
+            double ya[kTdChunk], yb[kTdChunk];
+            auto load = [&](double(&yk)[kTdChunk], int j0) {
+#pragma unroll
+                for (int k = 0; k < kTdChunk; k++) yk[k] = y[j0 + k];
+            };
+            int j = 0;
+            load(ya, 0);
+            for (; j + 2 * kTdChunk <= m; j += 2 * kTdChunk) {
+                load(yb, j + kTdChunk);
+                chunk(ya, j);
+                load(ya, j + 2 * kTdChunk);
+                chunk(yb, j + kTdChunk);
+            }
+            if (j + kTdChunk <= m) {
+                chunk(ya, j);
+                j += kTdChunk;
             }
             double bk[kTdChunk];
 #pragma unroll
@@ -1202,6 +1277,20 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
     return launched();
 }
 
+// warm-up length of td_ema_spec_kernel for the rule's contraction |1 - a|:
+// the smallest w with |1 - a|^w < 2^-64; 0 (no speculation) when the rule
+// does not contract or w would pass 2^20.  OTH_TD_SPEC_WARM overrides it
+// (tools/tests only: a tiny warm-up makes the guesses miss, which exercises
+// the rerun path).
+static int64_t td_spec_warm(double oma) {
+    if (const char* env = getenv("OTH_TD_SPEC_WARM")) return atoll(env);
+    const double c = fabs(oma);
+    if (!(c < 1.0)) return 0;
+    if (c == 0.0) return 1;
+    const double w = ceil(-64.0 * log(2.0) / log(c));
+    return w > (double)(1 << 20) ? 0 : (int64_t)w;
+}
+
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
                      int64_t n_long, void* stream) {
@@ -1213,8 +1302,13 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
                                                                          n_seg, long_min);
     int rc = launched();
     if (rc != OTH_OK || n_long == 0) return rc;
+    const int64_t warm = td_spec_warm(one_minus_a);
     td_ema_long_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
-                                                                         out, long_idx);
+                                                                         out, long_idx, warm);
+    rc = launched();
+    if (rc != OTH_OK || warm <= 0) return rc;
+    td_ema_spec_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
+                                                                         out, long_idx, warm);
     return launched();
 }
 

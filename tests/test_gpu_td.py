@@ -48,15 +48,20 @@ def test_state_map_at_scale_vs_oracle():
     assert torch.all(sm.keys[1:] > sm.keys[:-1])  # table stays sorted and unique
 
 
-@pytest.mark.parametrize("long_min", [None, 48, 1024])
-def test_td_ema_zero_states_in_long_segments(long_min):
+@pytest.mark.parametrize("long_min,spec_warm", [(None, None), (48, None), (1024, None), (48, "1"), (1024, "3")])
+def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
     """oth_td_ema speculates that no state in a 16-update chunk is exactly 0 and
     redoes the chunk otherwise: plant exact zero states (a = 0.5, x = -v) at
     chunk starts, middles and ends of long segments and compare with the
     sequential rule in Python floats.  With long_min, oth_td_ema_split runs
     the segments at least that long on a whole wave each (LDS stages of 1024
-    values: lengths around multiples of the stage)."""
+    values: lengths around multiples of the stage), those at least 4 warm-ups
+    long split into parts over the wave's lanes (warm-up 64 at a = 0.5).  A
+    warm-up of 1 or 3 values (OTH_TD_SPEC_WARM) makes most guesses miss: the
+    rerun path."""
     from subproc_amd import _lib
+    if spec_warm is not None:
+        monkeypatch.setenv("OTH_TD_SPEC_WARM", spec_warm)
     a, oma = 0.5, 0.5
     rng = np.random.default_rng(11)
     lengths = [1, 5, 47, 48, 49, 63, 64, 100, 1000, 1023, 1024, 1025, 2048, 4099, 12345]
@@ -87,6 +92,44 @@ def test_td_ema_zero_states_in_long_segments(long_min):
         _lib.check(lib.oth_td_ema_split(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
                                         len(lengths), long_min, li.data_ptr(), li.numel(), st), "oth_td_ema_split")
     assert out.cpu().tolist() == [w[1] for w in want]
+
+
+@pytest.mark.parametrize("kind", ["normal", "constant", "sparse"])
+def test_td_ema_split_speculation_learner_rate(kind):
+    """Long segments at the learner's rate (a = 0.03, warm-up 1457 values) split
+    over up to 64 lanes: the result is the sequential rule's, bit for bit,
+    whether the lanes' guesses converge (random targets), sit on a fixed
+    point of the rounding (a constant target) or run through exact zeros
+    (mostly-zero targets: draws)."""
+    from subproc_amd import _lib
+    a = 0.03
+    oma = 1 - a
+    rng = np.random.default_rng({"normal": 5, "constant": 6, "sparse": 7}[kind])
+    lengths = [5827, 5828, 9000, 70001, 200003]
+    vals, seg, want = [], [0], []
+    for L in lengths:
+        if kind == "normal":
+            xs = rng.normal(size=L) * 0.01
+        elif kind == "constant":
+            xs = np.full(L, 0.1234567)
+        else:
+            xs = np.where(rng.random(L) < 0.9, 0.0, rng.normal(size=L))
+        v = 0.0
+        for x in xs.tolist():
+            vals.append(x)
+            v = x if v == 0.0 else v * oma + x * a
+        seg.append(len(vals))
+        want.append(v)
+    dv = torch.tensor(vals, dtype=torch.float64, device=DEV)
+    ds = torch.tensor(seg, dtype=torch.int64, device=DEV)
+    init = torch.zeros(len(lengths), dtype=torch.float64, device=DEV)
+    out = torch.empty(len(lengths), dtype=torch.float64, device=DEV)
+    li = torch.arange(len(lengths), dtype=torch.int64, device=DEV)
+    lib = _lib.load()
+    _lib.check(lib.oth_td_ema_split(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
+                                    len(lengths), 1024, li.data_ptr(), li.numel(),
+                                    torch.cuda.current_stream().cuda_stream), "oth_td_ema_split")
+    assert out.cpu().tolist() == want
 
 
 def test_fit_on_device_matches_sklearn():

@@ -71,6 +71,8 @@ t = mark("td_ema_split", t)
 assert torch.equal(out, out2)
 print("long segments", long_idx.numel())
 print("max segment", int(counts.max()), "segments", ukeys.numel(), "updates", total)
+torch.cuda.synchronize()
+t = time.perf_counter()  # (the check and the prints above are not a stage)
 n_old, n_upd = len(sm), ukeys.numel()
 rank_in_upd = torch.searchsorted(ukeys, sm.keys)
 t = mark("m.ss_old_in_upd", t)

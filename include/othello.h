@@ -30,6 +30,7 @@
 #ifndef SUBPROC_AMD_OTHELLO_H
 #define SUBPROC_AMD_OTHELLO_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -199,6 +200,17 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
                      int64_t n_long, void* stream);
+
+/* The grouping sort between oth_td_updates and oth_td_ema: the n (key, value)
+ * pairs of the update stream into key order, stable (a key's values keep
+ * their stream order), keys_out/vals_out distinct from the inputs.  Keys must
+ * be OTH_TD_KEY values (non-negative, below 2^OTH_TD_KEY_BITS).  temp == NULL
+ * is a size query: *temp_bytes receives the scratch size (device memory, the
+ * caller's) for n pairs and nothing else happens; otherwise *temp_bytes is the
+ * size of temp.  Replaces the sort of the updates in learner order by key that
+ * __update_state_for_a_book's per-key EMA implies (37-62). */
+int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
+                      void* temp, size_t* temp_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -189,6 +189,40 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
 }
 
+/* stable sort of (key, value) pairs by key: bottom-up merge sort of the pair
+ * indices (temp holds 2 * n int64 indices), then a gather */
+int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
+                      void* temp, size_t* temp_bytes, void* stream) {
+    (void)stream;
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    const size_t need = (size_t)(n > 0 ? n : 1) * 2 * sizeof(int64_t);
+    if (!temp) {
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (*temp_bytes < need || (n > 0 && (!keys_in || !vals_in || !keys_out || !vals_out))) return OTH_EINVAL;
+    int64_t* a = (int64_t*)temp;
+    int64_t* b = a + n;
+    for (int64_t i = 0; i < n; i++) a[i] = i;
+    for (int64_t w = 1; w < n; w *= 2) {
+        for (int64_t lo = 0; lo < n; lo += 2 * w) {
+            const int64_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+            int64_t i = lo, j = mid, k = lo;
+            while (i < mid && j < hi) b[k++] = keys_in[a[j]] < keys_in[a[i]] ? a[j++] : a[i++]; /* ties: left first */
+            while (i < mid) b[k++] = a[i++];
+            while (j < hi) b[k++] = a[j++];
+        }
+        int64_t* t = a;
+        a = b;
+        b = t;
+    }
+    for (int64_t i = 0; i < n; i++) {
+        keys_out[i] = keys_in[a[i]];
+        vals_out[i] = vals_in[a[i]];
+    }
+    return OTH_OK;
+}
+
 int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
              void* stream) {
     (void)stream;

@@ -14,11 +14,14 @@ side (progress_position_moves_learn.py:37-62):
 Here the whole batch runs on the device:
   1. ``oth_td_updates`` (HIP) emits the ordered update stream: packed counts()
      key + value per (position, side), from an ``oth_replay`` position table;
-  2. a stable sort by key (torch) groups each key's updates in stream order;
-  3. ``oth_td_ema_split`` (HIP) replays each key's updates sequentially in
+  2. ``oth_td_sort_pairs`` (rocPRIM radix sort over the key's 54 bits) sorts
+     the (key, value) pairs by key, stably: each key's updates stay in stream
+     order;
+  3. ``oth_td_ema_split`` (HIP) replays each key's updates in order in
      float64 with separate multiply and add, so every value is bit-identical
      to the Python learner's (a key with at least LONG_MIN updates gets a
-     whole wavefront, which stages its values through LDS);
+     whole wavefront; the longest are split over its lanes from verified
+     warm-up guesses);
   4. the result is merged into the device-resident, key-sorted table.
 Batches applied one after another equal one batch of all their books.
 Values are kept as float64 (the Python learner's float, before any store
@@ -27,6 +30,8 @@ round trip).  ``StateMap.fit`` runs the learner's regression step
 a shard on the device instead of a random 50,000-state sample; Redis and the
 pyres fan-out stay out of scope.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -111,8 +116,14 @@ class StateMap:
             check(lib.oth_td_updates(pos_boards.contiguous().data_ptr(), plies.contiguous().data_ptr(),
                                      base.data_ptr(), self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n,
                                      stream), "oth_td_updates")
-            sk, perm = torch.sort(keys, stable=True)
-            sv = vals[perm].contiguous()
+            sk, sv = torch.empty_like(keys), torch.empty_like(vals)
+            tb = ctypes.c_size_t(0)
+            check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total, None,
+                                        ctypes.byref(tb), stream), "oth_td_sort_pairs")
+            temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=self.device)
+            check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total,
+                                        temp.data_ptr(), ctypes.byref(tb), stream), "oth_td_sort_pairs")
+            del temp
             ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
             seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
             torch.cumsum(counts, 0, out=seg_off[1:])

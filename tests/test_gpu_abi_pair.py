@@ -49,6 +49,43 @@ def same(*bufs):
         np.testing.assert_array_equal(b.device_as_host(), b.h)
 
 
+def sort_pair(keys, vals, keys_out, vals_out, n):
+    """oth_td_sort_pairs on both libraries, scratch sized by each one's query."""
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    st = torch.cuda.current_stream().cuda_stream
+    for lib, ptr, s in ((cpu, lambda b: HOSTP(b.h), None), (gpu, lambda b: b.d.data_ptr(), st)):
+        tb = ctypes.c_size_t(0)
+        assert lib.oth_td_sort_pairs(ptr(keys), ptr(vals), ptr(keys_out), ptr(vals_out), n, None,
+                                     ctypes.byref(tb), s) == 0
+        if lib is gpu:
+            temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=DEV)
+            tp = temp.data_ptr()
+        else:
+            temp = np.zeros(max(tb.value, 1), np.uint8)
+            tp = HOSTP(temp)
+        assert lib.oth_td_sort_pairs(ptr(keys), ptr(vals), ptr(keys_out), ptr(vals_out), n, tp, ctypes.byref(tb),
+                                     s) == 0
+    torch.cuda.synchronize()
+    same(keys_out, vals_out)
+
+
+@pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
+def test_td_sort_pairs_stable(n, distinct):
+    """Keys over all 54 key bits with many repeats: both builds sort stably (values
+    are the stream positions, so any reordering of equal keys shows)."""
+    rng = np.random.default_rng(n)
+    pool = rng.integers(0, 1 << 54, size=distinct, dtype=np.int64)
+    pool[0] = 0
+    pool[-1] = (1 << 54) - 1
+    k = pool[rng.integers(0, distinct, size=n)]
+    keys, vals = Buf(k), Buf(np.arange(n, dtype=np.float64))
+    ko, vo = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64))
+    sort_pair(keys, vals, ko, vo, n)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(ko.h, k[order])
+    np.testing.assert_array_equal(vo.h, order.astype(np.float64))
+
+
 def positions(n, seed):
     b, t, nt, m = (Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint8)),
                    Buf(np.zeros(n, np.uint8)))
@@ -134,6 +171,11 @@ def test_td_pair():
     order = np.argsort(keys.h, kind="stable")
     uk, starts = np.unique(keys.h[order], return_index=True)
     sv = Buf(vals.h[order])
+    # the grouping sort: both builds give numpy's stable order, bit for bit
+    sk2, sv2 = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+    sort_pair(keys, vals, sk2, sv2, total)
+    np.testing.assert_array_equal(sk2.h, keys.h[order])
+    np.testing.assert_array_equal(sv2.h.view(np.int64), sv.h.view(np.int64))
     seg = Buf(np.append(starts, total).astype(np.int64))
     init = Buf(np.random.default_rng(4).choice([0.0, 0.5, -1.25], len(uk)))
     out = Buf(np.zeros(len(uk), np.float64))
@@ -179,6 +221,12 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_eval(None, None, None, None, 0, s) == E
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 3, s) == E
         assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 0, None, 0, s) == E  # long_min < 1
+        tb = ctypes.c_size_t(0)
+        assert lib.oth_td_sort_pairs(None, None, None, None, 0, None, ctypes.byref(tb), s) == 0  # size query
+        assert lib.oth_td_sort_pairs(None, None, None, None, 0, ctypes.c_void_p(8), ctypes.byref(tb), s) == 0
+        assert lib.oth_td_sort_pairs(None, None, None, None, -1, None, ctypes.byref(tb), s) == E
+        assert lib.oth_td_sort_pairs(None, None, None, None, 5, None, None, s) == E  # no size
+        assert lib.oth_td_sort_pairs(None, None, None, None, 5, ctypes.c_void_p(8), ctypes.byref(tb), s) == E
     # every rollout output may be NULL: only the histogram is produced
     n = 4096
     hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))

@@ -56,8 +56,15 @@ def test_cpu_abi_td_matches_fixture_and_batches_compose():
         keys, vals = np.empty(int(cnt.sum()), np.int64), np.empty(int(cnt.sum()), np.float64)
         assert lib.oth_td_updates(P(np.ascontiguousarray(b)), P(np.ascontiguousarray(pl)), P(base), P(lam), P(keys),
                                   P(vals), n, None) == 0
+        # the grouping sort through the ABI (size query, then the sort), as StateMap.update
+        sk, sv = np.empty_like(keys), np.empty_like(vals)
+        tb = ctypes.c_size_t(0)
+        assert lib.oth_td_sort_pairs(P(keys), P(vals), P(sk), P(sv), len(keys), None, ctypes.byref(tb), None) == 0
+        temp = np.empty(tb.value, np.uint8)
+        assert lib.oth_td_sort_pairs(P(keys), P(vals), P(sk), P(sv), len(keys), P(temp), ctypes.byref(tb), None) == 0
         order = np.argsort(keys, kind="stable")
-        sk, sv = keys[order], np.ascontiguousarray(vals[order])
+        np.testing.assert_array_equal(sk, keys[order])
+        np.testing.assert_array_equal(sv, vals[order])
         uk, starts, counts = np.unique(sk, return_index=True, return_counts=True)
         seg = np.ascontiguousarray(np.append(starts, len(sk)).astype(np.int64))
         init = np.ascontiguousarray([state.get(int(k), 0.0) for k in uk], np.float64)

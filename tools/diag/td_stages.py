@@ -49,6 +49,20 @@ sk, perm = torch.sort(keys, stable=True)
 t = mark("sort", t)
 sv = vals[perm].contiguous()
 t = mark("gather", t)
+import ctypes  # noqa: E402
+lib = _lib.load()
+st = torch.cuda.current_stream().cuda_stream
+sk2, sv2 = torch.empty_like(keys), torch.empty_like(vals)
+tb = ctypes.c_size_t(0)
+_lib.check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk2.data_ptr(), sv2.data_ptr(), total, None,
+                                 ctypes.byref(tb), st), "q")
+temp = torch.empty(tb.value, dtype=torch.uint8, device=dev)
+t = mark("sort_pairs_alloc", t)
+_lib.check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk2.data_ptr(), sv2.data_ptr(), total,
+                                 temp.data_ptr(), ctypes.byref(tb), st), "s")
+t = mark("sort_pairs", t)
+assert torch.equal(sk, sk2) and torch.equal(sv, sv2)
+t = time.perf_counter()
 ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
 t = mark("unique", t)
 seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=dev)

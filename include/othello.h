@@ -212,6 +212,19 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
                       void* temp, size_t* temp_bytes, void* stream);
 
+/* The batch's results into the table: old_keys (n_old, unique, ascending) with
+ * old_vals, and upd_keys (n_upd, unique, ascending) with their new values
+ * upd_vals, merged into out_keys / out_vals, ascending; a key in both lists
+ * appears once, with its upd value.  new_before (n_upd + 1 entries) counts
+ * the batch keys absent from the table: new_before[j] = how many of
+ * upd_keys[0..j) are not in old_keys.  The output has n_old +
+ * new_before[n_upd] entries and must not overlap the inputs.  Keys are
+ * OTH_TD_KEY values.  This is the store write of every updated key
+ * (progress_position_moves_learn.py:58-62) for a whole batch. */
+int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                 const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                 double* out_vals, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -223,6 +223,30 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
     return OTH_OK;
 }
 
+/* the sorted union, batch values winning (two-pointer merge; new_before is
+ * the GPU kernel's placement input and is only bounds-checked here) */
+int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                 const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                 double* out_vals, void* stream) {
+    (void)stream;
+    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+        (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) || (n_old + n_upd > 0 && (!out_keys || !out_vals)))
+        return OTH_EINVAL;
+    const int64_t n_out = n_old + (n_upd > 0 ? new_before[n_upd] : 0);
+    int64_t i = 0, j = 0, k = 0;
+    while ((i < n_old || j < n_upd) && k < n_out) {
+        if (j >= n_upd || (i < n_old && old_keys[i] < upd_keys[j])) {
+            out_keys[k] = old_keys[i];
+            out_vals[k++] = old_vals[i++];
+        } else {
+            if (i < n_old && old_keys[i] == upd_keys[j]) i++;
+            out_keys[k] = upd_keys[j];
+            out_vals[k++] = upd_vals[j++];
+        }
+    }
+    return (i < n_old || j < n_upd || k != n_out) ? OTH_EINVAL : OTH_OK;
+}
+
 int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n,
              void* stream) {
     (void)stream;

@@ -1,0 +1,220 @@
+// td_table.hip — the TD state map's table work around the EMA
+// (progress_position_moves_learn.py:37-62 applies a batch's updates key by key,
+// in stream order, to the store):
+//   oth_td_sort_pairs: the update stream's (key, value) pairs in key order,
+//     stable, so each key's values stay in stream order;
+//   oth_td_merge: the batch's updated keys merged into the key-sorted table.
+//
+// The sort:
+// rocPRIM's onesweep radix sort of the pairs themselves over the key's 54 bits
+// (OTH_TD_KEY_BITS): 7 8-bit digit passes of 16-byte pairs.  torch.sort of the
+// keys with a permutation is 8 passes of (key, int64 index) pairs plus a gather
+// of the values by that permutation.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "../../include/othello.h"
+
+namespace {
+
+constexpr int kMergeBlock = 256;
+constexpr int kMergeK = 8;                               // merged positions per thread
+constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
+
+// The merge-path splits of the tile's two ends, found together by the block:
+// for diagonal d the split is the first i in [lo, hi] with A[i] >= B[d-i-1]
+// (A[i] < B[d-i-1] holds below it, fails from it on).  Each half of the block
+// searches one end: every round each of its nt threads probes one of nt evenly
+// spaced indices, and the count of probes that hold narrows the range to one
+// gap; a range of at most nt indices is probed at unit steps, which gives the
+// split.  ~4 rounds for 10^8 keys, instead of 27 dependent loads by one
+// thread.  Block-uniform: every thread runs every round.
+template <typename Key>
+__device__ void coop_splits(const Key* A, int64_t nA, const Key* B, int64_t nB, int64_t d0, int64_t d1,
+                            int64_t* split, int* cnt) {
+    const int nt = (int)blockDim.x / 2, g = (int)threadIdx.x / nt, t = (int)threadIdx.x - g * nt;
+    const int64_t d = g ? d1 : d0;
+    int64_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
+    bool done = false;
+    for (;;) {
+        const int64_t span = hi - lo;
+        const bool fine = span <= nt;
+        bool holds = false;
+        if (!done && span > 0) {
+            const int64_t i = fine ? lo + t : lo + span * (t + 1) / (nt + 1);
+            holds = (!fine || t < span) && A[i] < B[d - i - 1];
+        }
+        if (threadIdx.x == 0) cnt[0] = cnt[1] = 0;
+        __syncthreads();
+        if (holds) atomicAdd(&cnt[g], 1);
+        __syncthreads();
+        const int c = cnt[g];
+        if (!done) {
+            if (fine) {  // (span 0 included: c = 0)
+                if (t == 0) split[g] = lo + c;
+                done = true;
+            } else {
+                // probes 0..c-1 hold and probe c fails: the split is in (p(c-1), p(c)]
+                const int64_t nlo = c > 0 ? lo + span * c / (nt + 1) + 1 : lo;
+                const int64_t nhi = c < nt ? lo + span * (c + 1) / (nt + 1) : hi;
+                lo = nlo;
+                hi = nhi;
+            }
+        }
+        if (__syncthreads_and(done)) return;
+    }
+}
+
+// Merge path over the table (A: old keys, unique, sorted) and the batch's keys
+// (B: unique, sorted; their new values), one tile of the merged sequence per
+// block.  A table key equal to a batch key comes right after it and is
+// dropped; every other element lands at its merged position minus the drops
+// before it, which are the hits among the batch keys taken so far:
+//   hits_before(j) = j - new_before[j].
+// The block finds its tile's ends in A and B (two cooperative searches), stages
+// the tile's keys and values in LDS with coalesced loads, each thread finds its
+// own 8 positions by a search in LDS and merges them into registers, and the
+// block writes its outputs (one contiguous range) back through LDS, coalesced.
+__global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __restrict__ A,
+                                                               const double* __restrict__ Av, int64_t nA,
+                                                               const int64_t* __restrict__ B,
+                                                               const double* __restrict__ Bv,
+                                                               const int64_t* __restrict__ new_before, int64_t nB,
+                                                               int64_t* __restrict__ out_k,
+                                                               double* __restrict__ out_v) {
+    __shared__ int64_t sk[kMergeTile];
+    __shared__ double sv[kMergeTile];
+    __shared__ int64_t split[2];
+    __shared__ int cnt[2];
+    __shared__ unsigned long long range[2];  // min slot, max slot + 1 of the block's outputs
+    const int tid = threadIdx.x;
+    const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
+    const int64_t d1 = d0 + kMergeTile < nA + nB ? d0 + kMergeTile : nA + nB;
+    coop_splits(A, nA, B, nB, d0, d1, split, cnt);  // threads 0..127: the tile's start, 128..255: its end
+    if (tid == 0) {
+        range[0] = ~0ull;
+        range[1] = 0;
+    }
+    __syncthreads();
+    const int64_t a0 = split[0], b0 = d0 - a0;
+    const int na = (int)(split[1] - a0), nb = (int)(d1 - split[1] - b0);
+    for (int k = tid; k < na; k += kMergeBlock) {
+        sk[k] = A[a0 + k];
+        sv[k] = Av[a0 + k];
+    }
+    for (int k = tid; k < nb; k += kMergeBlock) {
+        sk[na + k] = B[b0 + k];
+        sv[na + k] = Bv[b0 + k];
+    }
+    __syncthreads();
+    const int n = na + nb;
+    const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
+    int lo = t0 > nb ? t0 - nb : 0, hi = t0 < na ? t0 : na;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sk[mid] < sk[na + t0 - mid - 1]) lo = mid + 1;
+        else hi = mid;
+    }
+    int i = lo, j = t0 - lo;
+    int64_t prev_b = t0 < t1 && b0 + j > 0 ? B[b0 + j - 1] : -1;  // keys are >= 0: -1 matches none
+    // (a caller's inconsistent new_before must not send a store out of bounds)
+    const uint64_t n_out = (uint64_t)(nA + new_before[nB]);
+    int64_t ok[kMergeK];
+    double ov[kMergeK];
+    uint64_t os[kMergeK];
+    unsigned long long smin = ~0ull, smax = 0;
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) {
+        os[q] = ~0ull;  // no output
+        const int m = t0 + q;
+        if (m >= t1) continue;
+        const int64_t gm = d0 + m;
+        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
+            const int64_t key = sk[i];
+            if (key != prev_b) {  // not the table copy of the batch key just taken
+                const int64_t bc = b0 + j;
+                os[q] = (uint64_t)(gm - (bc - new_before[bc]));
+                ok[q] = key;
+                ov[q] = sv[i];
+            }
+            i++;
+        } else {
+            const int64_t bj = b0 + j;
+            const int64_t key = sk[na + j];
+            os[q] = (uint64_t)(gm - (bj - new_before[bj]));
+            ok[q] = key;
+            ov[q] = sv[na + j];
+            prev_b = key;
+            j++;
+        }
+        if (os[q] >= n_out) os[q] = ~0ull;
+        if (os[q] != ~0ull) {
+            smin = min(smin, (unsigned long long)os[q]);
+            smax = max(smax, (unsigned long long)os[q] + 1);
+        }
+    }
+    if (smin != ~0ull) {
+        atomicMin(&range[0], smin);
+        atomicMax(&range[1], smax);
+    }
+    __syncthreads();  // every thread is done reading sk / sv
+    const unsigned long long base = range[0], end = range[1];
+    if (base == ~0ull) return;  // a tile whose only element was dropped
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) {
+        if (os[q] == ~0ull) continue;
+        sk[os[q] - base] = ok[q];
+        sv[os[q] - base] = ov[q];
+    }
+    __syncthreads();
+    const int cnt_out = (int)(end - base);  // <= kMergeTile: one slot per merged position at most
+    for (int k = tid; k < cnt_out; k += kMergeBlock) {
+        out_k[base + k] = sk[k];
+        out_v[base + k] = sv[k];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                 const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                 double* out_vals, void* stream) {
+    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+        (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) || (n_old + n_upd > 0 && (!out_keys || !out_vals)))
+        return OTH_EINVAL;
+    const int64_t n = n_old + n_upd;
+    if (n == 0) return OTH_OK;
+    td_merge_kernel<<<(unsigned)((n + kMergeTile - 1) / kMergeTile), kMergeBlock, 0, (hipStream_t)stream>>>(
+        old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
+                      void* temp, size_t* temp_bytes, void* stream) {
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    // the keys are non-negative and below 2^OTH_TD_KEY_BITS: as unsigned words
+    // their order is the signed order, and the bits above are all zero
+    const uint64_t* kin = reinterpret_cast<const uint64_t*>(keys_in);
+    uint64_t* kout = reinterpret_cast<uint64_t*>(keys_out);
+    if (!temp) {  // size query: no work, no launch
+        size_t bytes = 0;
+        const hipError_t e = rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
+                                                       OTH_TD_KEY_BITS, (hipStream_t)stream);
+        *temp_bytes = bytes;
+        return e == hipSuccess ? OTH_OK : -(int)e;
+    }
+    if (n > 0 && (!keys_in || !vals_in || !keys_out || !vals_out)) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    size_t bytes = *temp_bytes;
+    const hipError_t e = rocprim::radix_sort_pairs(temp, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
+                                                   OTH_TD_KEY_BITS, (hipStream_t)stream);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+}  // extern "C"

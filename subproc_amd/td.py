@@ -22,7 +22,8 @@ Here the whole batch runs on the device:
      to the Python learner's (a key with at least LONG_MIN updates gets a
      whole wavefront; the longest are split over its lanes from verified
      warm-up guesses);
-  4. the result is merged into the device-resident, key-sorted table.
+  4. ``oth_td_merge`` (HIP merge path) merges the result into the
+     device-resident, key-sorted table.
 Batches applied one after another equal one batch of all their books.
 Values are kept as float64 (the Python learner's float, before any store
 round trip).  ``StateMap.fit`` runs the learner's regression step
@@ -128,11 +129,12 @@ class StateMap:
             seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
             torch.cumsum(counts, 0, out=seg_off[1:])
             init = torch.zeros(ukeys.numel(), dtype=torch.float64, device=self.device)
-            pos_in_old = None
+            hit = None
             if len(self):
                 pos_in_old = torch.searchsorted(self.keys, ukeys)  # old keys < each update key
                 cl = pos_in_old.clamp(max=len(self) - 1)
-                init = torch.where(self.keys[cl] == ukeys, self.values[cl], init)
+                hit = self.keys[cl] == ukeys
+                init = torch.where(hit, self.values[cl], init)
             out = torch.empty_like(init)
             # keys with many updates (the opening and the first plies of every
             # game) are each run by a whole wavefront (oth_td_ema_split)
@@ -140,38 +142,30 @@ class StateMap:
             check(lib.oth_td_ema_split(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
                                        out.data_ptr(), ukeys.numel(), LONG_MIN, long_idx.data_ptr(),
                                        long_idx.numel(), stream), "oth_td_ema_split")
-            if pos_in_old is None:
+            if hit is None:
                 self.keys, self.values = ukeys, out
             else:
-                self._merge(pos_in_old, ukeys, out)
+                self._merge(hit, cl, ukeys, out, lib, stream)
         return total
 
-    def _merge(self, pos_in_old, ukeys, out):
-        """Merge the updated keys (sorted, unique) into the table (sorted) by
-        rank, with gathers and scatters only (no compaction, no re-sort):
-          old key i    -> slot i + (new keys below it)
-          update key j -> slot (new keys before j) + (old keys below it)
-        A key in both lists gets the same slot and the same (key, value) from
-        both sides, so the duplicate write is benign."""
+    def _merge(self, hit, cl, ukeys, out, lib, stream):
+        """The batch's keys (sorted, unique; hit: already in the table, at cl)
+        into the key-sorted table.  No new key: the values are scattered in
+        place.  Otherwise oth_td_merge (HIP merge path) writes the sorted
+        union, placing every element by rank; new_before[j] = batch keys
+        before j that are new."""
         n_old, n_upd = len(self), ukeys.numel()
-        rank_in_upd = torch.searchsorted(ukeys, self.keys)  # update keys < each old key
-        cl = rank_in_upd.clamp(max=n_upd - 1)
-        hit = ukeys[cl] == self.keys
         new_before = torch.zeros(n_upd + 1, dtype=torch.int64, device=self.device)
-        torch.cumsum((self.keys[pos_in_old.clamp(max=n_old - 1)] != ukeys).long(), 0, out=new_before[1:])
+        torch.cumsum(~hit, 0, out=new_before[1:])
         n_new = int(new_before[-1])
-        old_vals = torch.where(hit, out[cl], self.values)
         if n_new == 0:
-            self.values = old_vals
+            self.values[cl] = out
             return
-        pos_old = torch.arange(n_old, device=self.device) + new_before[rank_in_upd]
-        pos_upd = new_before[:-1] + pos_in_old
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
-        keys[pos_old] = self.keys
-        vals[pos_old] = old_vals
-        keys[pos_upd] = ukeys
-        vals[pos_upd] = out
+        check(lib.oth_td_merge(self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(), out.data_ptr(),
+                               new_before.data_ptr(), n_upd, keys.data_ptr(), vals.data_ptr(), stream),
+              "oth_td_merge")
         self.keys, self.values = keys, vals
 
     def update_from_books(self, books):

@@ -86,6 +86,33 @@ def test_td_sort_pairs_stable(n, distinct):
     np.testing.assert_array_equal(vo.h, order.astype(np.float64))
 
 
+@pytest.mark.parametrize("n_old,n_upd,overlap", [(0, 5, 0.0), (7, 0, 0.0), (1, 1, 1.0), (5000, 3000, 0.5),
+                                                  (300_000, 1_000_000, 0.3), (2_000_000, 40_000, 0.9),
+                                                  (100_000, 100_000, 1.0)])
+def test_td_merge_pair(n_old, n_upd, overlap):
+    """The table merge on both builds against numpy: sorted union, batch values
+    where a key is in both; tiles of 2,048 merged positions, so ties and runs of
+    one side cross tile and thread boundaries."""
+    rng = np.random.default_rng(n_old * 7 + n_upd)
+    old = np.unique(rng.integers(0, 1 << 54, size=n_old, dtype=np.int64))
+    n_hit = int(overlap * min(len(old), n_upd))
+    upd = np.unique(np.concatenate([rng.choice(old, size=n_hit, replace=False) if n_hit else old[:0],
+                                    rng.integers(0, 1 << 54, size=n_upd - n_hit, dtype=np.int64)]))
+    ov = rng.normal(size=len(old))
+    uv = rng.normal(size=len(upd))
+    new = ~np.isin(upd, old)
+    nb = np.concatenate([[0], np.cumsum(new)]).astype(np.int64)
+    n_out = len(old) + int(nb[-1])
+    want = dict(zip(old.tolist(), ov.tolist()))
+    want.update(zip(upd.tolist(), uv.tolist()))
+    ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
+    out_k, out_v = Buf(np.full(n_out, -7, np.int64)), Buf(np.zeros(n_out))
+    both("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
+    same(out_k, out_v)
+    assert out_k.h.tolist() == sorted(want)
+    assert out_v.h.tolist() == [want[k] for k in sorted(want)]
+
+
 def positions(n, seed):
     b, t, nt, m = (Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint8)),
                    Buf(np.zeros(n, np.uint8)))
@@ -227,6 +254,10 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_sort_pairs(None, None, None, None, -1, None, ctypes.byref(tb), s) == E
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, None, None, s) == E  # no size
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, ctypes.c_void_p(8), ctypes.byref(tb), s) == E
+        assert lib.oth_td_merge(None, None, 0, None, None, None, 0, None, None, s) == 0
+        assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, s) == E
+        assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, s) == E
+        assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, s) == E
     # every rollout output may be NULL: only the histogram is produced
     n = 4096
     hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))

@@ -103,3 +103,23 @@ def test_fit_matches_sklearn_on_fixture_states():
         lr = linear_model.LinearRegression(fit_intercept=True).fit(X, y)
         np.testing.assert_allclose(coef[k], lr.coef_, rtol=1e-6, atol=1e-9)
         np.testing.assert_allclose(icpt[k], lr.intercept_, rtol=1e-6, atol=1e-9)
+
+
+def test_cpu_abi_td_merge():
+    """The CPU build's table merge: sorted union, batch values where a key is in
+    both, and OTH_EINVAL when new_before does not add up."""
+    lib = oracle.cpu_abi()
+    rng = np.random.default_rng(3)
+    old = np.unique(rng.integers(0, 1 << 54, size=5000, dtype=np.int64))
+    upd = np.unique(np.concatenate([rng.choice(old, 1000, replace=False), rng.integers(0, 1 << 54, 2000)]))
+    ov, uv = rng.normal(size=len(old)), rng.normal(size=len(upd))
+    nb = np.concatenate([[0], np.cumsum(~np.isin(upd, old))]).astype(np.int64)
+    n_out = len(old) + int(nb[-1])
+    ok, vals = np.empty(n_out, np.int64), np.empty(n_out)
+    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals), None) == 0
+    want = dict(zip(old.tolist(), ov.tolist()))
+    want.update(zip(upd.tolist(), uv.tolist()))
+    assert ok.tolist() == sorted(want) and vals.tolist() == [want[k] for k in sorted(want)]
+    nb[-1] -= 1  # one new key too few: the output would overflow
+    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals),
+                            None) == _lib.OTH_EINVAL

@@ -109,4 +109,15 @@ vals[pos_old] = old_vals
 keys[pos_upd] = ukeys
 vals[pos_upd] = out
 t = mark("m.scatter", t)
+hit_u = sm.keys[pos_in_old.clamp(max=n_old - 1)] == ukeys
+nb2 = torch.zeros(n_upd + 1, dtype=torch.int64, device=dev)
+torch.cumsum(~hit_u, 0, out=nb2[1:])
+t = mark("k.cumsum", t)
+k2 = torch.empty(n_old + n_new, dtype=torch.int64, device=dev)
+v2 = torch.empty(n_old + n_new, dtype=torch.float64, device=dev)
+t = mark("k.alloc", t)
+_lib.check(lib.oth_td_merge(sm.keys.data_ptr(), sm.values.data_ptr(), n_old, ukeys.data_ptr(), out.data_ptr(),
+                            nb2.data_ptr(), n_upd, k2.data_ptr(), v2.data_ptr(), st), "m")
+t = mark("k.merge", t)
+assert torch.equal(k2, keys) and torch.equal(v2, vals)
 print({k: round(v, 2) for k, v in T.items()}, "total", round(sum(T.values()), 1))

@@ -212,6 +212,13 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
                       void* temp, size_t* temp_bytes, void* stream);
 
+/* The batch's keys in the table: old_keys (n_old, unique, ascending) with
+ * old_vals, upd_keys (n_upd, unique, ascending).  init[j] = the table value of
+ * upd_keys[j], 0.0 if absent (a fresh key reads as 0, 53-56); is_new[j] = 1
+ * if absent, else 0 (its cumsum is oth_td_merge's new_before). */
+int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                  int64_t n_upd, double* init, uint8_t* is_new, void* stream);
+
 /* The batch's results into the table: old_keys (n_old, unique, ascending) with
  * old_vals, and upd_keys (n_upd, unique, ascending) with their new values
  * upd_vals, merged into out_keys / out_vals, ascending; a key in both lists

@@ -223,6 +223,23 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
     return OTH_OK;
 }
 
+/* each batch key in the table by a two-pointer walk */
+int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                  int64_t n_upd, double* init, uint8_t* is_new, void* stream) {
+    (void)stream;
+    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+        (n_upd > 0 && (!upd_keys || !init || !is_new)))
+        return OTH_EINVAL;
+    int64_t i = 0;
+    for (int64_t j = 0; j < n_upd; j++) {
+        while (i < n_old && old_keys[i] < upd_keys[j]) i++;
+        const int hit = i < n_old && old_keys[i] == upd_keys[j];
+        init[j] = hit ? old_vals[i] : 0.0;
+        is_new[j] = (uint8_t)!hit;
+    }
+    return OTH_OK;
+}
+
 /* the sorted union, batch values winning (two-pointer merge; new_before is
  * the GPU kernel's placement input and is only bounds-checked here) */
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,

@@ -3,6 +3,8 @@
 // in stream order, to the store):
 //   oth_td_sort_pairs: the update stream's (key, value) pairs in key order,
 //     stable, so each key's values stay in stream order;
+//   oth_td_lookup: the batch's keys looked up in the key-sorted table (their
+//     states before the batch);
 //   oth_td_merge: the batch's updated keys merged into the key-sorted table.
 //
 // The sort:
@@ -177,9 +179,67 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     }
 }
 
+// The batch's keys (B) looked up in the table (A) by the same merge path:
+// a batch key at merged position m has the m - j table keys below it taken
+// before it, and is in the table iff the next table key equals it.  Every
+// batch key is written once, by the thread whose positions hold it.
+__global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* __restrict__ A,
+                                                                const double* __restrict__ Av, int64_t nA,
+                                                                const int64_t* __restrict__ B, int64_t nB,
+                                                                double* __restrict__ init,
+                                                                uint8_t* __restrict__ is_new) {
+    __shared__ int64_t sk[kMergeTile];
+    __shared__ int64_t split[2];
+    __shared__ int cnt[2];
+    const int tid = threadIdx.x;
+    const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
+    const int64_t d1 = d0 + kMergeTile < nA + nB ? d0 + kMergeTile : nA + nB;
+    coop_splits(A, nA, B, nB, d0, d1, split, cnt);
+    const int64_t a0 = split[0], b0 = d0 - a0;
+    const int na = (int)(split[1] - a0), nb = (int)(d1 - split[1] - b0);
+    for (int k = tid; k < na; k += kMergeBlock) sk[k] = A[a0 + k];
+    for (int k = tid; k < nb; k += kMergeBlock) sk[na + k] = B[b0 + k];
+    __syncthreads();
+    const int n = na + nb;
+    const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
+    int lo = t0 > nb ? t0 - nb : 0, hi = t0 < na ? t0 : na;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sk[mid] < sk[na + t0 - mid - 1]) lo = mid + 1;
+        else hi = mid;
+    }
+    int i = lo, j = t0 - lo;
+    for (int m = t0; m < t1; m++) {
+        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
+            i++;
+            continue;
+        }
+        // batch key b0 + j; the next table key is A[a0 + i] (past the tile: from HBM)
+        const int64_t key = sk[na + j], ai = a0 + i;
+        const int64_t next = i < na ? sk[i] : (ai < nA ? A[ai] : -1);
+        const bool hit = next == key;
+        init[b0 + j] = hit ? Av[ai] : 0.0;
+        is_new[b0 + j] = hit ? 0 : 1;
+        j++;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                  int64_t n_upd, double* init, uint8_t* is_new, void* stream) {
+    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+        (n_upd > 0 && (!upd_keys || !init || !is_new)))
+        return OTH_EINVAL;
+    if (n_upd == 0) return OTH_OK;
+    const int64_t n = n_old + n_upd;
+    td_lookup_kernel<<<(unsigned)((n + kMergeTile - 1) / kMergeTile), kMergeBlock, 0, (hipStream_t)stream>>>(
+        old_keys, old_vals, n_old, upd_keys, n_upd, init, is_new);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
 
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,

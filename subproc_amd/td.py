@@ -22,8 +22,10 @@ Here the whole batch runs on the device:
      to the Python learner's (a key with at least LONG_MIN updates gets a
      whole wavefront; the longest are split over its lanes from verified
      warm-up guesses);
-  4. ``oth_td_merge`` (HIP merge path) merges the result into the
-     device-resident, key-sorted table.
+  4. ``oth_td_lookup`` (before 3: each key's state before the batch) and
+     ``oth_td_merge`` (after it: the results into the device-resident,
+     key-sorted table) are HIP merge paths over the table and the batch's
+     keys.
 Batches applied one after another equal one batch of all their books.
 Values are kept as float64 (the Python learner's float, before any store
 round trip).  ``StateMap.fit`` runs the learner's regression step
@@ -128,13 +130,15 @@ class StateMap:
             ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
             seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
             torch.cumsum(counts, 0, out=seg_off[1:])
-            init = torch.zeros(ukeys.numel(), dtype=torch.float64, device=self.device)
-            hit = None
+            n_upd = ukeys.numel()
+            is_new = None
             if len(self):
-                pos_in_old = torch.searchsorted(self.keys, ukeys)  # old keys < each update key
-                cl = pos_in_old.clamp(max=len(self) - 1)
-                hit = self.keys[cl] == ukeys
-                init = torch.where(hit, self.values[cl], init)
+                init = torch.empty(n_upd, dtype=torch.float64, device=self.device)
+                is_new = torch.empty(n_upd, dtype=torch.uint8, device=self.device)
+                check(lib.oth_td_lookup(self.keys.data_ptr(), self.values.data_ptr(), len(self), ukeys.data_ptr(),
+                                        n_upd, init.data_ptr(), is_new.data_ptr(), stream), "oth_td_lookup")
+            else:
+                init = torch.zeros(n_upd, dtype=torch.float64, device=self.device)
             out = torch.empty_like(init)
             # keys with many updates (the opening and the first plies of every
             # game) are each run by a whole wavefront (oth_td_ema_split)
@@ -142,25 +146,21 @@ class StateMap:
             check(lib.oth_td_ema_split(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
                                        out.data_ptr(), ukeys.numel(), LONG_MIN, long_idx.data_ptr(),
                                        long_idx.numel(), stream), "oth_td_ema_split")
-            if hit is None:
+            if is_new is None:
                 self.keys, self.values = ukeys, out
             else:
-                self._merge(hit, cl, ukeys, out, lib, stream)
+                self._merge(is_new, ukeys, out, lib, stream)
         return total
 
-    def _merge(self, hit, cl, ukeys, out, lib, stream):
-        """The batch's keys (sorted, unique; hit: already in the table, at cl)
-        into the key-sorted table.  No new key: the values are scattered in
-        place.  Otherwise oth_td_merge (HIP merge path) writes the sorted
+    def _merge(self, is_new, ukeys, out, lib, stream):
+        """The batch's keys (sorted, unique; is_new: absent from the table) into
+        the key-sorted table: oth_td_merge (HIP merge path) writes the sorted
         union, placing every element by rank; new_before[j] = batch keys
         before j that are new."""
         n_old, n_upd = len(self), ukeys.numel()
         new_before = torch.zeros(n_upd + 1, dtype=torch.int64, device=self.device)
-        torch.cumsum(~hit, 0, out=new_before[1:])
+        torch.cumsum(is_new, 0, out=new_before[1:])
         n_new = int(new_before[-1])
-        if n_new == 0:
-            self.values[cl] = out
-            return
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
         check(lib.oth_td_merge(self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(), out.data_ptr(),

@@ -106,6 +106,13 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     want = dict(zip(old.tolist(), ov.tolist()))
     want.update(zip(upd.tolist(), uv.tolist()))
     ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
+    # the lookup that precedes the EMA: the batch keys' table values and new flags
+    init, is_new = Buf(np.full(len(upd), 9.0)), Buf(np.full(len(upd), 7, np.uint8))
+    both("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
+    same(init, is_new)
+    np.testing.assert_array_equal(is_new.h, new.astype(np.uint8))
+    olddict = dict(zip(old.tolist(), ov.tolist()))
+    assert init.h.tolist() == [olddict.get(k, 0.0) for k in upd.tolist()]
     out_k, out_v = Buf(np.full(n_out, -7, np.int64)), Buf(np.zeros(n_out))
     both("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
     same(out_k, out_v)
@@ -255,6 +262,9 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, None, None, s) == E  # no size
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, ctypes.c_void_p(8), ctypes.byref(tb), s) == E
         assert lib.oth_td_merge(None, None, 0, None, None, None, 0, None, None, s) == 0
+        assert lib.oth_td_lookup(None, None, 5, None, 0, None, None, s) == E  # table without pointers
+        assert lib.oth_td_lookup(None, None, 0, None, 0, None, None, s) == 0
+        assert lib.oth_td_lookup(None, None, 0, None, 3, None, None, s) == E
         assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, s) == E

@@ -123,3 +123,13 @@ def test_cpu_abi_td_merge():
     nb[-1] -= 1  # one new key too few: the output would overflow
     assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals),
                             None) == _lib.OTH_EINVAL
+
+
+def test_cpu_abi_td_lookup():
+    lib = oracle.cpu_abi()
+    old = np.array([2, 5, 9, 11], np.int64)
+    ov = np.array([0.5, -1.0, 2.0, 3.5])
+    upd = np.array([1, 5, 10, 11, 12], np.int64)
+    init, is_new = np.full(5, 9.0), np.full(5, 7, np.uint8)
+    assert lib.oth_td_lookup(P(old), P(ov), 4, P(upd), 5, P(init), P(is_new), None) == 0
+    assert init.tolist() == [0.0, -1.0, 0.0, 3.5, 0.0] and is_new.tolist() == [1, 0, 1, 0, 1]

@@ -119,5 +119,12 @@ t = mark("k.alloc", t)
 _lib.check(lib.oth_td_merge(sm.keys.data_ptr(), sm.values.data_ptr(), n_old, ukeys.data_ptr(), out.data_ptr(),
                             nb2.data_ptr(), n_upd, k2.data_ptr(), v2.data_ptr(), st), "m")
 t = mark("k.merge", t)
+init2 = torch.empty(n_upd, dtype=torch.float64, device=dev)
+isn = torch.empty(n_upd, dtype=torch.uint8, device=dev)
+t = time.perf_counter()
+_lib.check(lib.oth_td_lookup(sm.keys.data_ptr(), sm.values.data_ptr(), n_old, ukeys.data_ptr(), n_upd,
+                             init2.data_ptr(), isn.data_ptr(), st), "l")
+t = mark("k.lookup", t)
+assert torch.equal(init2, init) and torch.equal(isn.bool(), ~hit_u)
 assert torch.equal(k2, keys) and torch.equal(v2, vals)
 print({k: round(v, 2) for k, v in T.items()}, "total", round(sum(T.values()), 1))

@@ -824,14 +824,21 @@ __device__ __forceinline__ double td_run_full(double v, const double (&b)[kTdChu
     double y[kTdChunk];
 #pragma unroll
     for (int k = 0; k < kTdChunk; k++) y[k] = b[k] * a;
-    double w = v;
-    bool zero = false;
+    // each step: the chain's multiply, a running min of |state| (exactly 0
+    // iff some state was +-0; cheaper than a compare and an SGPR OR per
+    // step), the chain's add -- one asm block, so the min issues in the
+    // add's wait
+    double w = v, mn = 1.0;
 #pragma unroll
     for (int k = 0; k < kTdChunk; k++) {
-        zero |= (w == 0.0);
-        w = w * oma + y[k];
+        double t;
+        asm("v_mul_f64 %[t], %[w], %[oma]\n\t"
+            "v_min_f64 %[mn], %[mn], |%[w]|\n\t"
+            "v_add_f64 %[w], %[t], %[y]"
+            : [w] "+v"(w), [mn] "+v"(mn), [t] "=&v"(t)
+            : [oma] "v"(oma), [y] "v"(y[k]));
     }
-    return zero ? td_run(v, b, kTdChunk, a, oma) : w;
+    return mn == 0.0 ? td_run(v, b, kTdChunk, a, oma) : w;
 }
 // the rule over vals[i, e) from state v, one thread: short ranges step by
 // step; long ones software-pipelined (a ring of three chunks keeps 2 * kTdChunk
@@ -861,16 +868,27 @@ __device__ double td_range(double v, const double* __restrict__ vals, int64_t i,
     v = td_run(v, b2, r - 2 * kTdChunk, a, oma);
     return v;
 }
-// long_min: segments at least this long belong to td_ema_long_kernel (0: none)
+// long_min: segments at least this long belong to td_ema_long_kernel (0: none).
+// SHORT: every segment here is shorter than 3 chunks (long_min <= 3 * kTdChunk),
+// so the kernel has no ring of loads and needs a fraction of the registers:
+// more waves in flight for the millions of 1- to 3-update keys.
+template <bool SHORT>
 __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
                                                         const int64_t* __restrict__ seg_off,
                                                         const double* __restrict__ init, double a, double oma,
                                                         double* __restrict__ out, int64_t n_seg, int64_t long_min) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= n_seg) return;
-    const int64_t i = seg_off[s], e = seg_off[s + 1];
+    int64_t i = seg_off[s];
+    const int64_t e = seg_off[s + 1];
     if (long_min > 0 && e - i >= long_min) return;
-    out[s] = td_range(init ? init[s] : 0.0, vals, i, e, a, oma);
+    double v = init ? init[s] : 0.0;
+    if (SHORT) {
+        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
+        out[s] = v;
+    } else {
+        out[s] = td_range(v, vals, i, e, a, oma);
+    }
 }
 
 // Speculative split of a very long segment (the opening position's key gets
@@ -886,8 +904,10 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
 // matched has its lane's end state; one whose guess did not is rerun from the
 // verified state.  Every result is thus the sequential one; speculation only
 // decides how fast it comes.
+// (64 parts: 256 over a block of 4 waves measured slower, 0.80 against 0.73 ms
+// for the whole EMA of a 262,144-game batch)
 constexpr int kTdSpecLanes = 64;
-__global__ __launch_bounds__(64) void td_ema_spec_kernel(const double* __restrict__ vals,
+__global__ __launch_bounds__(kTdSpecLanes) void td_ema_spec_kernel(const double* __restrict__ vals,
                                                          const int64_t* __restrict__ seg_off,
                                                          const double* __restrict__ init, double a, double oma,
                                                          double* __restrict__ out,
@@ -898,8 +918,11 @@ __global__ __launch_bounds__(64) void td_ema_spec_kernel(const double* __restric
     const int64_t b = seg_off[s], e = seg_off[s + 1];
     const int64_t n = e - b;
     if (warm <= 0 || n < 4 * warm) return;  // td_ema_long_kernel's segment
-    const int parts = (int)min<int64_t>(kTdSpecLanes, n / (2 * warm));  // >= 2; every part >= 2 * warm long
-    const int64_t len = (n + parts - 1) / parts;
+    // parts of len >= 2 * warm values (a warm-up stays inside the segment and
+    // costs at most half a part), up to one per lane, none empty
+    const int64_t cap = min<int64_t>(kTdSpecLanes, n / (2 * warm));
+    const int64_t len = (n + cap - 1) / cap;
+    const int parts = (int)((n + len - 1) / len);
     if (lane < parts) {
         const int64_t i = b + lane * len, j = min(i + len, e);
         const double g = lane == 0 ? (init ? init[s] : 0.0) : td_range(0.0, vals, i - warm, i, a, oma);
@@ -1272,8 +1295,8 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
                double* out, int64_t n_seg, void* stream) {
     if (n_seg < 0 || (n_seg > 0 && (!values || !seg_off || !out))) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
-    td_ema_kernel<<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a, out,
-                                                                         n_seg, 0);
+    td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                one_minus_a, out, n_seg, 0);
     return launched();
 }
 
@@ -1298,8 +1321,12 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
         (n_seg > 0 && (!values || !seg_off || !out)) || (n_long > 0 && !long_idx))
         return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
-    td_ema_kernel<<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a, out,
-                                                                         n_seg, long_min);
+    if (long_min <= 3 * kTdChunk)
+        td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                   one_minus_a, out, n_seg, long_min);
+    else
+        td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                    one_minus_a, out, n_seg, long_min);
     int rc = launched();
     if (rc != OTH_OK || n_long == 0) return rc;
     const int64_t warm = td_spec_warm(one_minus_a);
@@ -1307,7 +1334,7 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
                                                                          out, long_idx, warm);
     rc = launched();
     if (rc != OTH_OK || warm <= 0) return rc;
-    td_ema_spec_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
+    td_ema_spec_kernel<<<(unsigned)n_long, kTdSpecLanes, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
                                                                          out, long_idx, warm);
     return launched();
 }

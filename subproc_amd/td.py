@@ -44,7 +44,7 @@ from .params import SHARDS
 
 A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
 LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
-LONG_MIN = 1024  # updates per key from which oth_td_ema_split runs the key on a whole wave
+LONG_MIN = 48  # updates per key from which oth_td_ema_split runs the key on a whole wave
 _SHIFTS = (47, 40, 35, 30, 25, 20, 15, 10, 5, 0)
 _WIDTH = (7, 7, 5, 5, 5, 5, 5, 5, 5, 5)
 

@@ -31,7 +31,9 @@ uk, counts = torch.unique_consecutive(sk, return_counts=True)
 seg = torch.zeros(uk.numel() + 1, dtype=torch.int64, device=dev)
 torch.cumsum(counts, 0, out=seg[1:])
 init = torch.zeros(uk.numel(), dtype=torch.float64, device=dev)
-li = torch.nonzero(counts >= td.LONG_MIN).flatten()
+LONG_MIN = int(os.environ.get("TD_LONG_MIN", td.LONG_MIN))
+li = torch.nonzero(counts >= LONG_MIN).flatten()
+print("long_min", LONG_MIN, "long segments", li.numel())
 for path in sys.argv[1:]:
     L = ctypes.CDLL(os.path.abspath(path))
     L.oth_td_ema_split.restype, L.oth_td_ema_split.argtypes = _lib.SIGNATURES["oth_td_ema_split"]
@@ -40,6 +42,6 @@ for path in sys.argv[1:]:
         torch.cuda.synchronize()
         t = time.perf_counter()
         L.oth_td_ema_split(sv.data_ptr(), seg.data_ptr(), init.data_ptr(), 0.03, 0.97, out.data_ptr(), uk.numel(),
-                           td.LONG_MIN, li.data_ptr(), li.numel(), st)
+                           LONG_MIN, li.data_ptr(), li.numel(), st)
         torch.cuda.synchronize()
         print("%-24s %.2f ms" % (os.path.basename(path), (time.perf_counter() - t) * 1e3))

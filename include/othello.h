@@ -212,6 +212,22 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,
                       void* temp, size_t* temp_bytes, void* stream);
 
+/* Sums for the learner's regression (fit_parameter,
+ * progress_position_moves_learn.py:160-184) over n states of one shard, keys
+ * (OTH_TD_KEY values) and values: x = counts()[1..9] of the key, y = value.
+ * mean == NULL (pass 1): row r of partials gets, for its share of the states,
+ *   [0] n, [1..9] sum x, [10] sum y.
+ * mean = (mean x[0..8], mean y) (pass 2): row r gets
+ *   [0..44] sum (x - mean x)(x - mean x)^T, upper triangle row by row,
+ *   [45..53] sum (x - mean x)(y - mean y).
+ * partials: OTH_TD_FIT_BLOCKS rows of OTH_TD_FIT_COLS doubles (device); the
+ * first 11 (pass 1) or 54 (pass 2) entries of every row are written, and the
+ * sum of the rows (in any fixed order) is the result. */
+#define OTH_TD_FIT_BLOCKS 1024
+#define OTH_TD_FIT_COLS 64
+int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, const double* mean,
+                       double* partials, void* stream);
+
 /* The batch's keys in the table: old_keys (n_old, unique, ascending) with
  * old_vals, upd_keys (n_upd, unique, ascending).  init[j] = the table value of
  * upd_keys[j], 0.0 if absent (a fresh key reads as 0, 53-56); is_new[j] = 1

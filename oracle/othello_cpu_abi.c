@@ -223,6 +223,32 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
     return OTH_OK;
 }
 
+/* the regression sums in one row (the other rows zero): same contract */
+int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, const double* mean, double* partials,
+                       void* stream) {
+    (void)stream;
+    if (n < 0 || !partials || (n > 0 && (!keys || !values))) return OTH_EINVAL;
+    memset(partials, 0, sizeof(double) * OTH_TD_FIT_BLOCKS * OTH_TD_FIT_COLS);
+    for (int64_t i = 0; i < n; i++) {
+        double x[9];
+        x[0] = (double)((keys[i] >> 40) & 127);
+        for (int r = 0; r < 8; r++) x[1 + r] = (double)((keys[i] >> (35 - 5 * r)) & 31);
+        if (!mean) {
+            partials[0] += 1.0;
+            for (int f = 0; f < 9; f++) partials[1 + f] += x[f];
+            partials[10] += values[i];
+        } else {
+            for (int f = 0; f < 9; f++) x[f] -= mean[f];
+            const double y = values[i] - mean[9];
+            int q = 0;
+            for (int f = 0; f < 9; f++)
+                for (int g = f; g < 9; g++) partials[q++] += x[f] * x[g];
+            for (int f = 0; f < 9; f++) partials[45 + f] += x[f] * y;
+        }
+    }
+    return OTH_OK;
+}
+
 /* each batch key in the table by a two-pointer walk */
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                   int64_t n_upd, double* init, uint8_t* is_new, void* stream) {

@@ -5,7 +5,8 @@
 //     stable, so each key's values stay in stream order;
 //   oth_td_lookup: the batch's keys looked up in the key-sorted table (their
 //     states before the batch);
-//   oth_td_merge: the batch's updated keys merged into the key-sorted table.
+//   oth_td_merge: the batch's updated keys merged into the key-sorted table;
+//   oth_td_fit_moments: the sums of the learner's per-shard regression.
 //
 // The sort:
 // rocPRIM's onesweep radix sort of the pairs themselves over the key's 54 bits
@@ -224,9 +225,97 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
     }
 }
 
+// Moments of the learner's regression over one shard's states (a contiguous
+// range of the key-sorted table: the phase is the key's top field).  x = the
+// 9 counts() features after the phase, y = the state value.  Pass 1 (mean ==
+// NULL): n, sum x, sum y.  Pass 2: the centred cross products sum (x - mx)(x -
+// mx)^T (upper triangle, 45) and sum (x - mx)(y - my) (9).  Each block leaves
+// its partial sums in its own row of `partials` (OTH_TD_FIT_COLS doubles); the
+// caller adds the OTH_TD_FIT_BLOCKS rows, in a fixed order: deterministic.
+constexpr int kFitBlock = 256;
+__device__ __forceinline__ void td_features(int64_t k, double (&x)[9]) {
+    x[0] = (double)((k >> 40) & 127);
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[1 + r] = (double)((k >> (35 - 5 * r)) & 31);
+}
+template <int NACC>
+__device__ __forceinline__ void block_sum_to_row(double (&acc)[NACC], double* row, double* lds) {
+    // wave sums by xor shuffles, then the block's waves through LDS
+#pragma unroll
+    for (int q = 0; q < NACC; q++) {
+        double v = acc[q];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[q] = v;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NACC; q++) lds[wave * NACC + q] = acc[q];
+    __syncthreads();
+    for (int q = threadIdx.x; q < NACC; q += blockDim.x) {
+        double v = 0.0;
+        for (int w = 0; w < kFitBlock / 64; w++) v += lds[w * NACC + q];
+        row[q] = v;
+    }
+}
+__global__ __launch_bounds__(kFitBlock) void td_fit_pass1_kernel(const int64_t* __restrict__ keys,
+                                                                 const double* __restrict__ vals, int64_t n,
+                                                                 double* __restrict__ partials) {
+    __shared__ double lds[(kFitBlock / 64) * 11];
+    double acc[11] = {};
+    for (int64_t i = (int64_t)blockIdx.x * kFitBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kFitBlock) {
+        double x[9];
+        td_features(keys[i], x);
+        acc[0] += 1.0;
+#pragma unroll
+        for (int f = 0; f < 9; f++) acc[1 + f] += x[f];
+        acc[10] += vals[i];
+    }
+    block_sum_to_row(acc, partials + (int64_t)blockIdx.x * OTH_TD_FIT_COLS, lds);
+}
+__global__ __launch_bounds__(kFitBlock) void td_fit_pass2_kernel(const int64_t* __restrict__ keys,
+                                                                 const double* __restrict__ vals, int64_t n,
+                                                                 const double* __restrict__ mean,
+                                                                 double* __restrict__ partials) {
+    __shared__ double lds[(kFitBlock / 64) * 54];
+    double mx[9];
+#pragma unroll
+    for (int f = 0; f < 9; f++) mx[f] = mean[f];
+    const double my = mean[9];
+    double acc[54] = {};
+    for (int64_t i = (int64_t)blockIdx.x * kFitBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kFitBlock) {
+        double x[9];
+        td_features(keys[i], x);
+#pragma unroll
+        for (int f = 0; f < 9; f++) x[f] -= mx[f];
+        const double y = vals[i] - my;
+        int q = 0;
+#pragma unroll
+        for (int f = 0; f < 9; f++)
+#pragma unroll
+            for (int g = f; g < 9; g++) acc[q++] += x[f] * x[g];
+#pragma unroll
+        for (int f = 0; f < 9; f++) acc[45 + f] += x[f] * y;
+    }
+    block_sum_to_row(acc, partials + (int64_t)blockIdx.x * OTH_TD_FIT_COLS, lds);
+}
+
 }  // namespace
 
 extern "C" {
+
+int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, const double* mean,
+                       double* partials, void* stream) {
+    if (n < 0 || !partials || (n > 0 && (!keys || !values))) return OTH_EINVAL;
+    if (mean)
+        td_fit_pass2_kernel<<<OTH_TD_FIT_BLOCKS, kFitBlock, 0, (hipStream_t)stream>>>(keys, values, n, mean,
+                                                                                      partials);
+    else
+        td_fit_pass1_kernel<<<OTH_TD_FIT_BLOCKS, kFitBlock, 0, (hipStream_t)stream>>>(keys, values, n, partials);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
 
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                   int64_t n_upd, double* init, uint8_t* is_new, void* stream) {

@@ -190,23 +190,38 @@ class StateMap:
         intercept of the state value on counts()[1:], states whose counts()[0]
         lies in the shard) over EVERY state of the map, not a random sample.
         Normal equations of the centred data, accumulated in float64 on the
-        device, solved (minimum norm) on the host.  Returns float64 arrays
+        device over the shard's contiguous range of the table by
+        oth_td_fit_moments (two passes: means, then centred cross products),
+        solved (minimum norm) on the host.  Returns float64 arrays
         coef (len(shards), 9), intercept (len(shards),), n (len(shards),)."""
-        c = unpack_counts(self.keys)
-        phase, X = c[:, 0], c[:, 1:].double()
-        coef = np.zeros((len(shards), X.shape[1]))
+        # the table is key-sorted and the phase is the key's top field: each
+        # shard is one contiguous range of it
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        edges = torch.tensor([[lo << _SHIFTS[0], (hi + 1) << _SHIFTS[0]] for lo, hi in shards], dtype=torch.int64,
+                             device=self.device)
+        ranges = torch.searchsorted(self.keys, edges.flatten()).view(-1, 2).cpu().tolist()
+        partials = torch.empty((_lib.TD_FIT_BLOCKS, _lib.TD_FIT_COLS), dtype=torch.float64, device=self.device)
+        coef = np.zeros((len(shards), 9))
         icpt = np.zeros(len(shards))
         nk = np.zeros(len(shards), np.int64)
-        for k, (lo, hi) in enumerate(shards):
-            m = (phase >= lo) & (phase <= hi)
-            Xk, yk = X[m], self.values[m]
-            nk[k] = Xk.shape[0]
+        for k, (s, e) in enumerate(ranges):
+            nk[k] = e - s
             if nk[k] == 0:
                 continue
-            xm, ym = Xk.mean(0), yk.mean()
-            Xc = Xk - xm
-            A = (Xc.T @ Xc).cpu().numpy()
-            b = (Xc.T @ (yk - ym)).cpu().numpy()
-            coef[k] = np.linalg.lstsq(A, b, rcond=None)[0]
-            icpt[k] = float(ym) - float(xm.cpu().numpy() @ coef[k])
+            kp, vp = self.keys[s:e], self.values[s:e]
+            with torch.cuda.device(self.device):
+                check(lib.oth_td_fit_moments(kp.data_ptr(), vp.data_ptr(), e - s, None, partials.data_ptr(), stream),
+                      "oth_td_fit_moments")
+                m1 = partials[:, :11].sum(0)
+                mean = torch.cat([m1[1:10], m1[10:11]]) / m1[0]
+                check(lib.oth_td_fit_moments(kp.data_ptr(), vp.data_ptr(), e - s, mean.data_ptr(),
+                                             partials.data_ptr(), stream), "oth_td_fit_moments")
+                m2 = partials[:, :54].sum(0).cpu().numpy()
+            A = np.zeros((9, 9))
+            A[np.triu_indices(9)] = m2[:45]
+            A = A + np.triu(A, 1).T
+            mean = mean.cpu().numpy()
+            coef[k] = np.linalg.lstsq(A, m2[45:54], rcond=None)[0]
+            icpt[k] = float(mean[9]) - float(mean[:9] @ coef[k])
         return coef, icpt, nk

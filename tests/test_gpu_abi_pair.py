@@ -120,6 +120,35 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     assert out_v.h.tolist() == [want[k] for k in sorted(want)]
 
 
+@pytest.mark.parametrize("n", [1, 1000, 3_000_001])
+def test_td_fit_moments_pair(n):
+    """The regression sums on both builds: the GPU's 1,024 block rows add up to
+    the CPU's single row, both passes; exact for the count and the integer
+    feature sums.  The float64 sums run in another order: the CPU's one
+    sequential sum of 3M terms carries ~n * eps of rounding, so rtol 1e-8 and
+    an absolute floor of 1e-10 of the largest sum (cross products near 0)."""
+    rng = np.random.default_rng(n)
+    keys = np.sort(rng.integers(0, 1 << 54, size=n, dtype=np.int64))
+    vals = rng.normal(size=n)
+    kb, vb = Buf(keys), Buf(vals)
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    st = torch.cuda.current_stream().cuda_stream
+    rows = (_lib.TD_FIT_BLOCKS, _lib.TD_FIT_COLS)
+    pd, ph = torch.zeros(rows, dtype=torch.float64, device=DEV), np.zeros(rows)
+    mean = None
+    for width in (11, 54):
+        m = None if mean is None else Buf(mean)
+        assert cpu.oth_td_fit_moments(HOSTP(kb.h), HOSTP(vb.h), n, None if m is None else HOSTP(m.h), HOSTP(ph),
+                                      None) == 0
+        assert gpu.oth_td_fit_moments(kb.d.data_ptr(), vb.d.data_ptr(), n, None if m is None else m.d.data_ptr(),
+                                      pd.data_ptr(), st) == 0
+        g, c = pd[:, :width].sum(0).cpu().numpy(), ph[:, :width].sum(0)
+        np.testing.assert_allclose(g, c, rtol=1e-8, atol=1e-10 * np.abs(c).max())
+        if width == 11:
+            np.testing.assert_array_equal(g[:10], c[:10])  # counts and integer feature sums: exact
+            mean = np.append(c[1:10], c[10]) / c[0]
+
+
 def positions(n, seed):
     b, t, nt, m = (Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.uint8)), Buf(np.zeros(n, np.uint8)),
                    Buf(np.zeros(n, np.uint8)))
@@ -265,6 +294,8 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_lookup(None, None, 5, None, 0, None, None, s) == E  # table without pointers
         assert lib.oth_td_lookup(None, None, 0, None, 0, None, None, s) == 0
         assert lib.oth_td_lookup(None, None, 0, None, 3, None, None, s) == E
+        assert lib.oth_td_fit_moments(None, None, 3, None, ctypes.c_void_p(8), s) == E
+        assert lib.oth_td_fit_moments(None, None, 0, None, None, s) == E  # no partials
         assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, s) == E

@@ -80,18 +80,37 @@ def test_cpu_abi_td_matches_fixture_and_batches_compose():
 
 
 def test_fit_matches_sklearn_on_fixture_states():
-    """StateMap.fit == sklearn LinearRegression(fit_intercept=True) per shard
-    (fit_parameter, progress_position_moves_learn.py:160-184) on the same
-    states; float64, tolerance rtol 1e-6 / atol 1e-9 on the coefficients."""
-    import torch
+    """StateMap.fit's algorithm through the CPU build of oth_td_fit_moments
+    (shard = contiguous range of the key-sorted table; pass 1 means, pass 2
+    centred cross products; minimum-norm solve) == sklearn
+    LinearRegression(fit_intercept=True) per shard (fit_parameter,
+    progress_position_moves_learn.py:160-184) on the same states; float64,
+    tolerance rtol 1e-6 / atol 1e-9 on the coefficients."""
     from sklearn import linear_model
 
     f = fixture()
-    sm = td.StateMap("cpu")
-    keys = sorted(td.counts_to_key(k) for k in f)
-    sm.keys = torch.tensor(keys, dtype=torch.int64)
-    sm.values = torch.tensor([f[td.key_to_counts(k)] for k in keys], dtype=torch.float64)
-    coef, icpt, n = sm.fit()
+    lib = oracle.cpu_abi()
+    keys = np.array(sorted(td.counts_to_key(k) for k in f), np.int64)
+    vals = np.array([f[td.key_to_counts(k)] for k in keys.tolist()], np.float64)
+    part = np.zeros((_lib.TD_FIT_BLOCKS, _lib.TD_FIT_COLS))
+    coef, icpt, n = np.zeros((4, 9)), np.zeros(4), np.zeros(4, np.int64)
+    for k, (lo, hi) in enumerate(td.SHARDS):
+        s, e = np.searchsorted(keys, [lo << 47, (hi + 1) << 47])
+        n[k] = e - s
+        if e == s:
+            continue
+        kp, vp = np.ascontiguousarray(keys[s:e]), np.ascontiguousarray(vals[s:e])
+        assert lib.oth_td_fit_moments(P(kp), P(vp), e - s, None, P(part), None) == 0
+        m1 = part[:, :11].sum(0)
+        assert m1[0] == e - s
+        mean = np.ascontiguousarray(np.append(m1[1:10], m1[10]) / m1[0])
+        assert lib.oth_td_fit_moments(P(kp), P(vp), e - s, P(mean), P(part), None) == 0
+        m2 = part[:, :54].sum(0)
+        A = np.zeros((9, 9))
+        A[np.triu_indices(9)] = m2[:45]
+        A = A + np.triu(A, 1).T
+        coef[k] = np.linalg.lstsq(A, m2[45:], rcond=None)[0]
+        icpt[k] = mean[9] - mean[:9] @ coef[k]
     assert n.sum() == len(keys)
     for k, (lo, hi) in enumerate(td.SHARDS):
         rows = [(c, v) for c, v in f.items() if lo <= c[0] <= hi]

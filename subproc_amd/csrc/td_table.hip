@@ -338,6 +338,14 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
         return OTH_EINVAL;
     const int64_t n = n_old + n_upd;
     if (n == 0) return OTH_OK;
+    if (n_upd == 0) {  // the table unchanged (new_before may be NULL: the kernel reads it)
+        hipError_t e = hipMemcpyAsync(out_keys, old_keys, (size_t)n_old * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                                      (hipStream_t)stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_vals, old_vals, (size_t)n_old * sizeof(double), hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream);
+        return e == hipSuccess ? OTH_OK : -(int)e;
+    }
     td_merge_kernel<<<(unsigned)((n + kMergeTile - 1) / kMergeTile), kMergeBlock, 0, (hipStream_t)stream>>>(
         old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals);
     const hipError_t e = hipGetLastError();

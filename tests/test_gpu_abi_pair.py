@@ -299,6 +299,13 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, s) == E
         assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, s) == E
+    # a batch with no keys: the table is copied, new_before is not needed (NULL)
+    old = Buf(np.array([3, 8, 40], np.int64))
+    ov = Buf(np.array([0.5, -2.0, 7.25]))
+    ok, ovo = Buf(np.zeros(3, np.int64)), Buf(np.zeros(3))
+    both("oth_td_merge", old, ov, 3, None, None, None, 0, ok, ovo)
+    same(ok, ovo)
+    assert ok.h.tolist() == [3, 8, 40] and ovo.h.tolist() == [0.5, -2.0, 7.25]
     # every rollout output may be NULL: only the histogram is produced
     n = 4096
     hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))

@@ -244,6 +244,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
     bufs = [(torch.empty((n, 2), dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int8, device=dev),
              torch.empty(n, dtype=torch.uint8, device=dev)) for _ in streams]
+    # one work word per stream (include/othello.h: 0 before and after each launch)
+    works = torch.zeros(len(streams), dtype=torch.int64, device=dev)
     lib = _lib.load()
     pid = {"random": 0, "greedy": 1, "eval": 2}[policy]
     wptr = None
@@ -253,12 +255,12 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
 
         wptr = _weights_ptr(DEFAULT_WEIGHTS)  # the learner's default table
 
-    def launch(gid, fb, df, pl, h, st):
+    def launch(gid, fb, df, pl, h, w, st):
         if policy == "eval":
             return lib.oth_rollout_eval(None, None, args.seed, gid, 10, wptr, fb.data_ptr(), df.data_ptr(),
-                                        pl.data_ptr(), None, h.data_ptr(), n, st.cuda_stream)
+                                        pl.data_ptr(), None, h.data_ptr(), w.data_ptr(), n, st.cuda_stream)
         return lib.oth_rollout(None, None, args.seed, gid, pid, 10, fb.data_ptr(), df.data_ptr(), pl.data_ptr(), None,
-                               h.data_ptr(), n, st.cuda_stream)
+                               h.data_ptr(), w.data_ptr(), n, st.cuda_stream)
 
     pending = []
     # per-launch events on the launch's own stream (the roofline's launch duration)
@@ -272,7 +274,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
         h = hists[s]
         if k is not None and LAUNCH_EVENTS:
             l0[k].record(st)
-        _lib.check(launch(bench_game_id0(s, rank, world, n), fb, df, pl, h, st), "rollout")
+        w = works[s % nstreams:s % nstreams + 1]
+        _lib.check(launch(bench_game_id0(s, rank, world, n), fb, df, pl, h, w, st), "rollout")
         if k is not None and LAUNCH_EVENTS:
             l1[k].record(st)
         if use_dist and args.allreduce != "end":
@@ -306,7 +309,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     t_w = time.perf_counter()
     while (time.perf_counter() - t_w) * 1e3 < args.prewarm_ms:
         fb, df, pl = bufs[0]
-        _lib.check(launch(1 << 52, fb, df, pl, scratch, stream), "rollout")
+        _lib.check(launch(1 << 52, fb, df, pl, scratch, works[0:1], stream), "rollout")
         torch.cuda.synchronize()
     fork()
     for s in range(args.warmup):
@@ -339,6 +342,11 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     timed = hists[args.warmup:].sum(0).cpu()  # already global (all-reduced) when distributed
     env_steps = int(timed[132])
     games = n * world * args.steps
+    # self-check of the sharding: every game of every rank is in the reduced
+    # histogram exactly once (its 129 diff bins and its W/L/D bins)
+    counted = int(timed[:129].sum())
+    if counted != games or int(timed[129:132].sum()) != games:
+        raise SystemExit(f"bench: the reduced histogram counts {counted} games, expected {games}")
     out = dict(metric="env-steps/sec (batched self-play)", value=env_steps / elapsed, unit="env-steps/s",
                n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
                higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u64",
@@ -347,7 +355,9 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
                config={"workload": "config%s: %s-policy self-play rollouts to terminal" %
                        ({"random": "3" if world == 1 else "4", "greedy": "5", "eval": " §8f"}[policy], policy),
                        "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
-                       "streams": nstreams, "env_steps_per_game": env_steps / games})
+                       "streams": nstreams, "env_steps_per_game": env_steps / games, "world_size": world,
+                       "game_ids": _game_id_ranges(n, world, args.warmup, args.steps),
+                       "games_counted": counted})
     # roofline: algorithmic bytes of one launch / that launch's duration (events on its stream)
     achieved = n * ROLLOUT_BYTES_PER_GAME / (launch_ms * 1e-3) / 1e9
     kname = "rollout_kernel<%d, false>" % pid
@@ -367,6 +377,19 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
         va = prof["SQ_INSTS_VALU"] / (step_ms * 1e-3)
         out["valu"] = valu_entry(kname, va, instr_per_launch=prof["SQ_INSTS_VALU"])
     return out
+
+
+def _game_id_ranges(n, world, warmup, steps):
+    """The global game ids each rank plays in the timed steps (dist.bench_game_id0):
+    step s on rank r plays [(s*world + r)*n, +n); listed per rank as its first
+    and last timed range, with the rule, so an N-GPU line is self-describing."""
+    from subproc_amd.dist import bench_game_id0
+
+    first, last = warmup, warmup + steps - 1
+    return {"rule": "step s on rank r: [(s*%d + r)*%d, +%d), timed steps s = %d..%d" % (world, n, n, first, last),
+            "per_rank": {str(r): [[bench_game_id0(first, r, world, n), bench_game_id0(first, r, world, n) + n],
+                                  [bench_game_id0(last, r, world, n), bench_game_id0(last, r, world, n) + n]]
+                         for r in range(world)}}
 
 
 def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks, launches=None, index0=0):
@@ -486,10 +509,14 @@ def _cpu_baseline(args, workload):
     import oracle
 
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count()
-    threads = max(1, min(16, cores))
+        affinity = os.cpu_count()
+    # every core of the affinity mask, capped by OMP_NUM_THREADS where the
+    # environment sets it (the GPU box sets 16: its CPU share per GPU)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(affinity, int(omp))) if omp and omp.isdigit() else affinity
+    host = {"nproc": os.cpu_count(), "affinity_cores": affinity, "omp_num_threads": omp}
     if workload == "step":
         pos = oracle.sample_midgame(65536, args.seed)
         t0 = time.perf_counter()
@@ -497,7 +524,7 @@ def _cpu_baseline(args, workload):
         for _ in range(reps):
             oracle.step(pos["boards"], pos["turn"], pos["move"])
         dt = time.perf_counter() - t0
-        return {"value": 65536 * reps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+        return {"value": 65536 * reps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", **host,
                 "sample": "%d x oracle_step over 65,536 mid-game positions" % reps}
     games = args.cpu_games
     pid = 0 if workload == "random" else 1
@@ -507,7 +534,7 @@ def _cpu_baseline(args, workload):
     r = oracle.rollout(games, args.seed, 0, pid, 10, n_threads=threads)
     dt = time.perf_counter() - t0
     steps = int(r["hist"][132])
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", **host,
             "sample": "%d %s games from the opening (%d env-steps), C mailbox restatement of board.py, "
                       "OpenMP %d threads, %.2f s wall" % (games, workload, steps, threads, dt),
             "board_py_note": "board.py itself (Python) measured at ~2.9e3 env-steps/s/core in the build container "

@@ -41,8 +41,12 @@ int main(int argc, char** argv) {
     int64_t* hist;
     CK(hipMalloc(&fb, n * 16));
     CK(hipMalloc(&hist, OTH_HIST_BINS * sizeof(int64_t)));
+    uint64_t* work;  // the rollouts' batch counter: zeroed once, left at 0 by every launch
+    CK(hipMalloc(&work, sizeof(uint64_t)));
+    CK(hipMemsetAsync(work, 0, sizeof(uint64_t), st));
     CK(hipMemsetAsync(hist, 0, OTH_HIST_BINS * sizeof(int64_t), st));
-    OTH(oth_rollout(nullptr, nullptr, seed, 0, OTH_POLICY_RANDOM, 0, fb, nullptr, nullptr, nullptr, hist, n, st));
+    OTH(oth_rollout(nullptr, nullptr, seed, 0, OTH_POLICY_RANDOM, 0, fb, nullptr, nullptr, nullptr, hist, work, n,
+                    st));
 
     // one batched step on the opening: every game plays d3 (square 19)
     uint64_t* boards;

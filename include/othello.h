@@ -12,17 +12,18 @@
  * Conventions:
  *   board   = 2 x uint64 per game, [black, white] (colour-absolute), array (n,2)
  *             bit sq = x + 8*y, x = file a..h, y = rank 1..8   (board.py:74-81)
- *   turn    = uint8, 1 = Black, 2 = White                         (board.py:3-7)
+ *   turn    = uint8, 1 = Black, 2 = White                         (board.py:3-7);
+ *             0 = Empty (deserialize with a side string other than 'O'/'X',
+ *             board.py:245-262), any other value = a piece no square holds
  *   move    = uint8 code, 0..63 = square, 64 = pass ('PS')      (board.py:192-209)
  *   legal   = uint64 bitboard; LSB-first order == puttables() row-major order
  *
  * Ownership / errors / threading:
  *   - every pointer is DEVICE memory owned by the caller (e.g. torch tensors);
- *     the library allocates nothing persistent;
+ *     the library allocates nothing and keeps no device state (the rollouts'
+ *     work counter is a word the caller passes in, see oth_rollout);
  *   - calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
- *     and thread-safe on distinct streams; they may be captured in a hipGraph
- *     (a captured rollout resets its own work counter on every replay); up to
- *     64 rollouts (and 64 captured ones) may execute concurrently;
+ *     and thread-safe on distinct streams; they may be captured in a hipGraph;
  *   - return value: OTH_OK (0), OTH_EINVAL (invalid argument, nothing launched),
  *     or -(hipError_t) of the failed launch.  Per-game semantics (illegal
  *     move ...) are reported in `ret`, never as a status.
@@ -71,16 +72,22 @@ const char* oth_version(void);
 int oth_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n, void* stream);
 
 /* Board.puttables(turn) (board.py:46-52) as a bitmask per game;
- * Board.n_puttable_for (54-55) = popcount.  turn outside {1,2} -> legal = 0. */
+ * Board.n_puttable_for (54-55) = popcount.  turn 0 (Empty) -> puttables(Empty):
+ * empty squares from which a run of Black discs ends on an empty square
+ * (hostile(Empty) = Black, 155-159); any other turn outside {1,2} -> 0. */
 int oth_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int64_t n, void* stream);
 
 /* Board.put_s (board.py:192-209) on integer move codes, one step per game:
  *   move == 64            -> ret 0, turn toggles (accepted even with legal moves)
  *   move 0..63, legal     -> ret = number of flipped discs (>= 1), board updated, turn toggles
  *   move 0..63, occupied or flips nothing -> ret -1, board and turn unchanged
- *   move > 64 or turn not in {1,2}         -> ret -1, unchanged  (board.py raises
- *                                              IndexError for 'a9')
- * Outputs: boards_out (n,2), turn_out, flips (discs flipped, origin excluded),
+ *   move > 64             -> ret -1, unchanged  (board.py raises IndexError for
+ *                            'a9'/'i1', the strings no code 0..64 stands for)
+ * "Toggles" is board.py's rule: Black -> White, anything else -> Black.  With
+ * turn 0 (Empty) a move flips the Black runs that end on an empty square to
+ * Empty (the origin stays empty); with any other turn outside {1,2} no move
+ * flips anything (only a pass is accepted).
+ * Outputs: boards_out (n,2), turn_out, flips (discs that changed, origin excluded),
  * legal_next = puttables(turn_out) on boards_out, ret.  Any output may be NULL.
  * boards_out may alias boards_in and turn_out may alias turn_in (in-place step).
  * nturn (may be NULL) is incremented in place where ret >= 0 (board.py:203-204). */
@@ -93,19 +100,38 @@ int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* m
 int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff,
                uint8_t* terminal, int64_t n, void* stream);
 
+/* Board.hands_for_direc (board.py:124-139) from any origin (x[i], y[i]) along
+ * any direction (dx[i], dy[i]) -- on the board, next to it or anywhere --
+ * with own[i] = the squares holding the piece and hostile[i] = the squares
+ * holding hostile(piece) (155-159).  count[i] = the length of the returned
+ * list; its entries are the squares (x + k*dx, y + k*dy) for k = 1..count[i].
+ * Off-board origins are what Python's list indexing lets Board.put /
+ * is_puttable_at reach (x = -1 is file h for the emptiness test while the scan
+ * starts at x = -1); a run of 8 hostile squares is kept without a closing
+ * piece, as board.py's 8-step loop does. */
+int oth_hands(const uint64_t* own, const uint64_t* hostile, const int64_t* x, const int64_t* y, const int64_t* dx,
+              const int64_t* dy, uint8_t* count, int64_t n, void* stream);
+
 /* Play n independent games to terminal (game_runner.py:165-201 loop, engines
  * replaced by `policy`; a side without a legal move passes).
- *   start / start_turn : (n,2) / (n) start positions; NULL = opening, Black to move
+ *   start / start_turn : (n,2) / (n) start positions; NULL = opening, Black to
+ *                        move; a start_turn other than 2 (White) is Black
  *   seed, game_id0     : game i uses the RNG stream of global game id game_id0 + i
  *                         -> results independent of batch split / GPU count
  *   policy, n_random   : OTH_POLICY_RANDOM, or OTH_POLICY_GREEDY whose first
  *                        n_random plies are random
  * Outputs (each may be NULL): final_boards (n,2), diff (n), plies (n) = env-steps
  * incl. passes, moves (n * OTH_MOVES_STRIDE, 255-padded move codes),
- * hist (OTH_HIST_BINS int64, ACCUMULATED: caller zeroes it). */
+ * hist (OTH_HIST_BINS int64, ACCUMULATED: caller zeroes it).
+ *   work : ONE device uint64 owned by the caller (required): the launch's
+ *          batch counter.  It must be 0 when the launch starts; the launch
+ *          leaves it 0 when it completes.  So a word zeroed once serves any
+ *          number of launches ordered on one stream (or replays of a graph),
+ *          and launches that may run concurrently need distinct words.  After
+ *          a failed or aborted launch, zero it again. */
 int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                 int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
-                uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+                uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream);
 
 /* oth_rollout with the eval policy: after n_random random plies, each mover
  * plays the legal move whose child maximises oth_eval(child, mover) under
@@ -114,7 +140,7 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
  * outputs as oth_rollout. */
 int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                      int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
-                     uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+                     uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream);
 
 /* A match between two eval tables (the GPU counterpart of GameRunner playing
  * engine A as Black against engine B as White, game_runner.py:154-201): as
@@ -123,7 +149,8 @@ int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t 
  * launch).  oth_rollout_eval(w) == oth_rollout_match(w, w). */
 int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                       int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
-                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream);
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n,
+                      void* stream);
 
 /* Synthetic reachable mid-game positions for the step benchmark (config 2):
  * position index0+j is a random-policy playout of 10..49 plies from the opening

@@ -60,12 +60,14 @@ def lib():
         L.oracle_features.argtypes = [P, P, P, I64]
         L.oracle_eval.argtypes = [P, P, P, P, I64]
         L.oracle_replay.argtypes = [P, P, P, P, P, P, P, I64]
+        L.oracle_hands.argtypes = [P, P, P, P, P, P, P, I64]
+        L.oracle_rollout_ids.argtypes = [P, I64, U64, I, I, P, P, P, P, P]
         L.oracle_game_key.argtypes = [U64, U64]
         L.oracle_game_key.restype = U64
         L.oracle_rng_draws.argtypes = [U64, ctypes.c_uint32]
         L.oracle_rng_draws.restype = ctypes.c_uint32
         for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
-                  "oracle_sample_midgame", "oracle_features", "oracle_eval", "oracle_replay"):
+                  "oracle_sample_midgame", "oracle_features", "oracle_eval", "oracle_replay", "oracle_hands", "oracle_rollout_ids"):
             getattr(L, f).restype = I
         _lib = L
     return _lib
@@ -147,6 +149,21 @@ def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=N
     return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h)
 
 
+def rollout_ids(ids, seed, policy=0, n_random=10, weights=None, weights_white=None):
+    """The games of global ids `ids` (any order / stride) from the opening, as
+    oracle_rollout plays them: dict(final_boards, diff, plies)."""
+    ids = np.ascontiguousarray(ids, np.uint64)
+    n = len(ids)
+    w = None if weights is None else _weights(weights)
+    ww = None if weights_white is None else _weights(weights_white)
+    fb = np.empty((n, 2), np.uint64)
+    d = np.empty(n, np.int8)
+    pl = np.empty(n, np.uint8)
+    rc = lib().oracle_rollout_ids(_p(ids), n, seed, policy, n_random, _p(w), _p(ww), _p(fb), _p(d), _p(pl))
+    assert rc == 0
+    return dict(final_boards=fb, diff=d, plies=pl)
+
+
 def sample_midgame(n, seed, index0=0):
     b = np.empty((n, 2), np.uint64)
     t, nt, m = (np.empty(n, np.uint8) for _ in range(3))
@@ -181,6 +198,18 @@ def replay(moves, plies, start=None, start_turn=None):
     e = np.zeros((n, MOVES_STRIDE + 1), np.uint8)
     lib().oracle_replay(_p(start), _p(st), _p(moves), _p(plies), _p(pos), _p(t), _p(e), n)
     return dict(boards=pos, turn=t, end=e)
+
+
+def hands(boards, piece, x, y, dx, dy):
+    """len(hands_for_direc((dx, dy), piece, x, y)) per item (board.py:124-139):
+    piece any 0..255, origin and direction any int64.  (n,) uint8."""
+    boards = _boards(boards)
+    n = len(boards)
+    piece = np.ascontiguousarray(np.broadcast_to(piece, n), np.uint8)
+    x, y, dx, dy = (np.ascontiguousarray(np.broadcast_to(v, n), np.int64) for v in (x, y, dx, dy))
+    out = np.empty(n, np.uint8)
+    lib().oracle_hands(_p(boards), _p(piece), _p(x), _p(y), _p(dx), _p(dy), _p(out), n)
+    return out
 
 
 def serialize_str(black, white, turn):

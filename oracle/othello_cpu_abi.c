@@ -34,6 +34,9 @@ int oracle_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weigh
 int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
                   uint64_t* pos, uint8_t* pos_turn, uint8_t* pos_end, int64_t n);
 
+int oracle_hands(const uint64_t* boards, const uint8_t* piece, const int64_t* x, const int64_t* y, const int64_t* dx,
+                 const int64_t* dy, uint8_t* count, int64_t n);
+
 const char* oth_version(void) { return "subproc_amd-cpu 0.1.0 host (oracle)"; }
 
 int oth_reset(uint64_t* boards, uint8_t* turn, uint8_t* nturn, int64_t n, void* stream) {
@@ -63,11 +66,26 @@ int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_
     return oracle_result(boards, n_black, n_white, diff, terminal, n);
 }
 
+/* own -> White squares, hostile -> Black squares, then the scan of piece White
+ * (hostile(White) = Black): the same question on a board the oracle holds */
+int oth_hands(const uint64_t* own, const uint64_t* hostile, const int64_t* x, const int64_t* y, const int64_t* dx,
+              const int64_t* dy, uint8_t* count, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!own || !hostile || !x || !y || !dx || !dy || !count))) return OTH_EINVAL;
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t b[2] = {hostile[i], own[i] & ~hostile[i]};
+        const uint8_t piece = OTH_WHITE;
+        oracle_hands(b, &piece, x + i, y + i, dx + i, dy + i, count + i, 1);
+    }
+    return OTH_OK;
+}
+
+/* `work` is the GPU launch's batch counter: checked, otherwise unused here */
 int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                 int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist,
-                int64_t n, void* stream) {
+                uint64_t* work, int64_t n, void* stream) {
     (void)stream;
-    if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
+    if (n < 0 || !work || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return oracle_rollout(start, start_turn, seed, game_id0, policy, n_random, final_boards, diff, plies, moves, hist,
                           n, 0, NULL, NULL);
@@ -75,9 +93,9 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
 
 int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                      int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
-                     uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+                     uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream) {
     (void)stream;
-    if (n < 0 || !weights) return OTH_EINVAL;
+    if (n < 0 || !weights || !work) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return oracle_rollout(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, final_boards, diff, plies,
                           moves, hist, n, 0, weights, NULL);
@@ -85,9 +103,10 @@ int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t 
 
 int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                       int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
-                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n,
+                      void* stream) {
     (void)stream;
-    if (n < 0 || !weights_black || !weights_white) return OTH_EINVAL;
+    if (n < 0 || !weights_black || !weights_white || !work) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return oracle_rollout(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, final_boards, diff, plies,
                           moves, hist, n, 0, weights_black, weights_white);

@@ -207,7 +207,7 @@ int oracle_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, i
     for (int64_t i = 0; i < n; i++) {
         Board s;
         board_from_bits(&s, boards[2 * i], boards[2 * i + 1], turn[i]);
-        legal[i] = (turn[i] == Black || turn[i] == White) ? puttables(&s, turn[i]) : 0;
+        legal[i] = puttables(&s, turn[i]); /* any piece value, as board.py (Empty: hostile = Black) */
     }
     return 0;
 }
@@ -220,8 +220,7 @@ int oracle_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t
         uint64_t b0 = boards_in[2 * i], w0 = boards_in[2 * i + 1];
         int t = turn_in[i];
         board_from_bits(&s, b0, w0, t);
-        int r = -1;
-        if (t == Black || t == White) r = put_code(&s, move[i]);
+        int r = put_code(&s, move[i]); /* any side to move, as board.py */
         uint64_t bl, wh;
         board_to_bits(&s, &bl, &wh);
         if (boards_out) {
@@ -229,9 +228,9 @@ int oracle_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t
             boards_out[2 * i + 1] = wh;
         }
         if (turn_out) turn_out[i] = (uint8_t)s.turn;
-        /* flipped discs = opponent discs that changed colour (origin excluded) */
-        if (flips) flips[i] = (t == Black) ? (w0 & ~wh) : (t == White) ? (b0 & ~bl) : 0;
-        if (legal_next) legal_next[i] = (s.turn == Black || s.turn == White) ? puttables(&s, s.turn) : 0;
+        /* flipped discs = squares that changed (origin excluded) */
+        if (flips) flips[i] = ((b0 ^ bl) | (w0 ^ wh)) & ~(move[i] < 64 ? 1ull << move[i] : 0ull);
+        if (legal_next) legal_next[i] = puttables(&s, s.turn);
         if (ret) ret[i] = (int8_t)r;
         if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1); /* board.py:203-204 */
     }
@@ -346,7 +345,10 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
 #pragma omp for schedule(dynamic, 64)
         for (int64_t i = 0; i < n; i++) {
             Board s;
-            if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
+            /* the build's rollouts start with Black or White to move (include/othello.h) */
+            if (start)
+                board_from_bits(&s, start[2 * i], start[2 * i + 1],
+                                start_turn && start_turn[i] == White ? White : Black);
             else board_init(&s);
             if (moves) memset(moves + i * MOVES_STRIDE, 255, MOVES_STRIDE);
             int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random, weights, weights_white,
@@ -369,6 +371,26 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     }
     if (hist)
         for (int k = 0; k < HIST_BINS; k++) hist[k] += h[k];
+    return 0;
+}
+
+/* the games of explicit global ids (a strided sample of a large launch): game
+ * j is the game oracle_rollout plays as id ids[j], from the opening */
+int oracle_rollout_ids(const uint64_t* ids, int64_t n, uint64_t seed, int policy, int n_random,
+                       const int8_t* weights, const int8_t* weights_white, uint64_t* final_boards, int8_t* diff,
+                       uint8_t* plies) {
+    if (policy == 2 && !weights) return -1;
+    if (!weights_white) weights_white = weights;
+    uint64_t S = seed_state(seed);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t j = 0; j < n; j++) {
+        Board s;
+        board_init(&s);
+        int p = play_game(&s, game_key(S, ids[j]), policy, n_random, weights, weights_white, 0);
+        board_to_bits(&s, &final_boards[2 * j], &final_boards[2 * j + 1]);
+        diff[j] = (int8_t)(n_of(&s, Black) - n_of(&s, White));
+        plies[j] = (uint8_t)p;
+    }
     return 0;
 }
 
@@ -445,8 +467,44 @@ int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_
             if (pos_turn) pos_turn[r] = (uint8_t)s.turn;
             if (pos_end) pos_end[r] = (uint8_t)is_game_over(&s);
             if (p == np) break;
-            if (s.turn == Black || s.turn == White) put_code(&s, moves[i * MOVES_STRIDE + p]);
+            put_code(&s, moves[i * MOVES_STRIDE + p]);
         }
+    }
+    return 0;
+}
+
+/* one step of a scan from coordinate c along d: false if it leaves the board
+ * (an overflowing coordinate is far off it) */
+static int step_on(int64_t c, int64_t d, int k, int64_t* out) {
+    int64_t t;
+    return !__builtin_mul_overflow(d, (int64_t)k, &t) && !__builtin_add_overflow(c, t, out) && *out >= 0 && *out < 8;
+}
+
+/* hands_for_direc (board.py:124-139) for any direc (dx, dy), piece and origin:
+ * the length of the returned list (its squares are steps 1..len) */
+static int hands_any(const Board* s, int64_t dx, int64_t dy, int piece, int64_t x, int64_t y) {
+    int n = 0, h = hostile(piece);
+    for (int i = 1; i < 9; i++) {
+        int64_t nx, ny;
+        int on = step_on(x, dx, i, &nx) && step_on(y, dy, i, &ny);
+        if (on && s->b[ny][nx] == h) {
+            n++;
+        } else if (on && s->b[ny][nx] == piece) {
+            break;
+        } else {
+            n = 0;
+            break;
+        }
+    }
+    return n;
+}
+
+int oracle_hands(const uint64_t* boards, const uint8_t* piece, const int64_t* x, const int64_t* y, const int64_t* dx,
+                 const int64_t* dy, uint8_t* count, int64_t n) {
+    for (int64_t i = 0; i < n; i++) {
+        Board s;
+        board_from_bits(&s, boards[2 * i], boards[2 * i + 1], Black);
+        count[i] = (uint8_t)hands_any(&s, dx[i], dy[i], piece[i], x[i], y[i]);
     }
     return 0;
 }

@@ -31,13 +31,14 @@ SIGNATURES = {
     "oth_legal": (_I, [_P, _P, _P, _I64, _P]),
     "oth_step": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_result": (_I, [_P, _P, _P, _P, _P, _I64, _P]),
-    "oth_rollout": (_I, [_P, _P, _U64, _U64, _I, _I, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_hands": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_rollout": (_I, [_P, _P, _U64, _U64, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_sample_midgame": (_I, [_U64, _U64, _P, _P, _P, _P, _I64, _P]),
     "oth_replay": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_book_text": (_I, [_P, _P, _I64, _P, _P]),
     "oth_features": (_I, [_P, _P, _P, _I64, _P]),
-    "oth_rollout_eval": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _I64, _P]),
-    "oth_rollout_match": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_rollout_eval": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_rollout_match": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_eval": (_I, [_P, _P, _P, _P, _I64, _P]),
     "oth_td_updates": (_I, [_P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),

@@ -4,20 +4,34 @@ served by the MI355X kernels.
 Callers of the reference (game_runner.py:3, learn_base.py:1, parameter.py:2)
 run unchanged with ``sys.modules['board'] = subproc_amd.board``.
 Same method names, argument order, colour values (Empty 0, Black 1, White 2),
-return codes and Edax move strings.
+return codes, Edax move strings -- and the same answers on every input
+board.py accepts, including the ones its plain-list implementation lets
+through:
 
-The rules themselves — legal moves, flips, pass/terminal, disc counts — are
-computed by the HIP library (one batch-of-one launch per call, through
-subproc_amd.ops); this class keeps only the two bitboards, the side to move and
-the ply counter on the host, plus the text codecs.  For throughput use the
-batched :class:`subproc_amd.env.VecEnv` / :mod:`subproc_amd.ops` instead.
+* the side to move (or a ``piece``) may be Empty or any other value:
+  hostile(piece) is Black unless piece is Black (board.py:155-159), so with
+  Empty to move the Black runs that end on an empty square are "flipped" to
+  Empty, and ``put_s`` then hands the turn to Black (205-208);
+* coordinates index ``board[y][x]`` like Python lists: -8..-1 wrap for the
+  emptiness test and the placed piece, while the ray scan starts from the
+  coordinate as given (an off-board origin next to the edge scans into the
+  board); ``hands_for_direc`` takes any origin and any direction;
+* ``board`` is a live ``board[y][x]`` view: writing through it changes the
+  game, as writing into board.py's list-of-lists does;
+* a square may hold a value other than Empty/Black/White (``set``): it then
+  blocks rays like board.py's cell would and ends the runs of a piece equal
+  to it.
 
-Documented deviations:
-  * ``put``/``hands_for_direc``/``is_puttable_at`` with an off-board (x, y),
-    including negative ones that Python list indexing would wrap, raise IndexError;
-  * a side to move other than Black/White (only reachable via deserialize of a
-    turn string other than 'O'/'X') makes ``put_s`` return -1 for every move.
+The rules -- legal moves, flips, pass/terminal, disc counts -- are computed by
+the HIP library (one batch-of-one launch per call, through subproc_amd.ops):
+``oth_legal`` / ``oth_step`` / ``oth_result`` for a board of Black, White and
+empty squares, ``oth_hands`` (any origin, any direction, any own/hostile
+squares) for the rest.  This class keeps the two bitboards, any other cell
+values, the side to move and the ply counter on the host, plus the text
+codecs.  For throughput use :class:`subproc_amd.env.VecEnv` / :mod:`subproc_amd.ops`.
 """
+import operator
+
 import numpy as np
 
 from . import codec
@@ -32,6 +46,8 @@ DIRECS = (LU, U, RU, L, R, LD, D, RD) = [  # board.py:9-17
 
 _OPEN_BLACK = 0x0000000810000000  # board.py:25  e4, d5
 _OPEN_WHITE = 0x0000001008000000  # board.py:24  d4, e5
+_M64 = (1 << 64) - 1
+_I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
 
 
 def _i64(x):
@@ -39,7 +55,24 @@ def _i64(x):
 
 
 def _u64(x):
-    return x & ((1 << 64) - 1)
+    return x & _M64
+
+
+def _popcount(x):
+    return bin(x & _M64).count("1")
+
+
+def _side_code(piece):
+    """The C-ABI side code of a piece value (include/othello.h): 1 / 2 / 0, and
+    3 for a value equal to none of them (a piece no square of a Black/White/
+    Empty board holds).  Decided with board.py's own == comparisons."""
+    if piece == Black:
+        return Black
+    if piece == White:
+        return White
+    if piece == Empty:
+        return Empty
+    return 3
 
 
 class _Device:
@@ -69,8 +102,8 @@ class _Device:
         self.turn.copy_(h[2:3], non_blocking=True)
         self.move.copy_(h[3:4], non_blocking=True)
 
-    def legal(self, black, white, piece):
-        self._load(black, white, piece)
+    def legal(self, black, white, code):
+        self._load(black, white, code)
         return _u64(int(self.ops.legal(self.boards, self.turn).item()))
 
     def result(self, black, white):
@@ -79,11 +112,21 @@ class _Device:
         t = self.torch.stack([r.n_black.long(), r.n_white.long(), r.terminal.long()]).view(-1).tolist()
         return t[0], t[1], bool(t[2])
 
-    def step(self, black, white, turn, code):
-        self._load(black, white, turn, code)
+    def step(self, black, white, code, move):
+        self._load(black, white, code, move)
         r = self.ops.step(self.boards, self.turn, self.move, want_legal=False)
         v = self.torch.cat([r.boards.view(-1), r.flips, r.ret.long()]).tolist()
         return _u64(v[0]), _u64(v[1]), _u64(v[2]), int(v[3])
+
+    def hands(self, own, hostile, rows):
+        """rows: [(x, y, dx, dy), ...] with one own/hostile pair -> run lengths."""
+        t = self.torch
+        n = len(rows)
+        a = t.tensor([[_i64(own), _i64(hostile), *r] for r in rows], dtype=t.int64).t().contiguous()
+        a = a.pin_memory().to(self.dev, non_blocking=True)
+        out = self.ops.hands(a[0].contiguous(), a[1].contiguous(), a[2].contiguous(), a[3].contiguous(),
+                             a[4].contiguous(), a[5].contiguous())
+        return out.cpu().tolist()[:n]
 
 
 _DEV = None
@@ -96,17 +139,112 @@ def _device():
     return _DEV
 
 
-def _check_xy(x, y):
-    if not (0 <= x < 8 and 0 <= y < 8):
+def _index(i):
+    """A list index as board.py's ``board[y][x]`` takes it: integers (or
+    __index__ objects) in -8..7, negative ones wrapping; else IndexError."""
+    i = operator.index(i)
+    if not -8 <= i < 8:
         raise IndexError("list index out of range")
+    return i % 8
+
+
+def _coord(c):
+    """An origin / direction component for the scan: any integer (bounded to
+    int64: every value past that is far off the board, and so is the bound)."""
+    c = operator.index(c)
+    return min(max(c, _I64_MIN), _I64_MAX)
+
+
+class _Row:
+    """``board[y]``: a live row of the board (board.py:23's inner list)."""
+
+    __slots__ = ("_b", "_y")
+
+    def __init__(self, b, y):
+        self._b, self._y = b, y
+
+    def __len__(self):
+        return 8
+
+    def __getitem__(self, x):
+        if isinstance(x, slice):
+            return [self._b._cell(i + 8 * self._y) for i in range(8)][x]
+        return self._b._cell(_index(x) + 8 * self._y)
+
+    def __setitem__(self, x, v):
+        if isinstance(x, slice):
+            xs = range(8)[x]
+            vs = list(v)
+            if len(vs) != len(xs):
+                raise ValueError("a board row has 8 squares: a slice assignment must keep its length")
+            for i, c in zip(xs, vs):
+                self._b._set_cell(i + 8 * self._y, c)
+            return
+        self._b._set_cell(_index(x) + 8 * self._y, v)
+
+    def __iter__(self):
+        return iter(self[:])
+
+    def __eq__(self, other):
+        try:
+            return list(self) == list(other)
+        except TypeError:
+            return NotImplemented
+
+    def __repr__(self):
+        return repr(list(self))
+
+
+class _Rows:
+    """``board``: the live list-of-lists view ``board[y][x]`` (board.py:23)."""
+
+    __slots__ = ("_b",)
+
+    def __init__(self, b):
+        self._b = b
+
+    def __len__(self):
+        return 8
+
+    def __getitem__(self, y):
+        if isinstance(y, slice):
+            return [_Row(self._b, i) for i in range(8)[y]]
+        return _Row(self._b, _index(y))
+
+    def __setitem__(self, y, row):
+        if isinstance(y, slice):
+            ys = range(8)[y]
+            rows = list(row)
+            if len(rows) != len(ys):
+                raise ValueError("the board has 8 rows: a slice assignment must keep its length")
+            for i, r in zip(ys, rows):
+                self[i] = r
+            return
+        cells = list(row)
+        if len(cells) != 8:
+            raise ValueError("a board row has 8 squares")
+        _Row(self._b, _index(y))[:] = cells
+
+    def __iter__(self):
+        return (_Row(self._b, i) for i in range(8))
+
+    def __eq__(self, other):
+        try:
+            return [list(r) for r in self] == [list(r) for r in other]
+        except TypeError:
+            return NotImplemented
+
+    def __repr__(self):
+        return repr([list(r) for r in self])
 
 
 class Board:
-    """board.py:20 — one game; hot-path methods run on the GPU."""
+    """board.py:20 -- one game; the rules run on the GPU."""
 
     def __init__(self):  # board.py:22-27
         self._black = _OPEN_BLACK
         self._white = _OPEN_WHITE
+        self._other = {}  # square -> a value equal to none of Empty/Black/White
         self.turn = Black
         self.nturn = 0
         self._cache = {}
@@ -114,19 +252,32 @@ class Board:
     # ---------------------------------------------------------------- state
     @property
     def board(self):
-        """list-of-lists view ``board[y][x]`` (a fresh copy, board.py:23)."""
-        return [[self.get(x, y) for x in range(8)] for y in range(8)]
+        """The live ``board[y][x]`` view (board.py:23): reads and writes go to this game."""
+        return _Rows(self)
 
     @board.setter
     def board(self, rows):
-        bl = wh = 0
-        for y in range(8):
-            for x in range(8):
-                c = rows[y][x]
-                if c == Black:
-                    bl |= 1 << (x + 8 * y)
-                elif c == White:
-                    wh |= 1 << (x + 8 * y)
+        rows = list(rows)
+        if len(rows) != 8:
+            raise ValueError("the board has 8 rows")
+        _Rows(self)[:] = rows
+
+    def _cell(self, sq):
+        if sq in self._other:
+            return self._other[sq]
+        return Black if self._black >> sq & 1 else White if self._white >> sq & 1 else Empty
+
+    def _set_cell(self, sq, piece):
+        bit = 1 << sq
+        bl, wh = self._black & ~bit, self._white & ~bit
+        self._other.pop(sq, None)
+        code = _side_code(piece)
+        if code == Black:
+            bl |= bit
+        elif code == White:
+            wh |= bit
+        elif code == 3:
+            self._other[sq] = piece
         self._set_bits(bl, wh)
 
     def _set_bits(self, black, white):
@@ -138,19 +289,43 @@ class Board:
         return self._black, self._white
 
     def set(self, piece, x, y):  # board.py:60-61
-        _check_xy(x, y)
-        bit = 1 << (x + 8 * y)
-        bl, wh = self._black & ~bit, self._white & ~bit
-        if piece == Black:
-            bl |= bit
-        elif piece == White:
-            wh |= bit
-        self._set_bits(bl, wh)
+        self._set_cell(self._sq(x, y), piece)
 
     def get(self, x, y):  # board.py:63-64
-        _check_xy(x, y)
-        sq = x + 8 * y
-        return Black if self._black >> sq & 1 else White if self._white >> sq & 1 else Empty
+        return self._cell(self._sq(x, y))
+
+    @staticmethod
+    def _sq(x, y):
+        # board[y][x]: the row index is taken first, as Python evaluates it
+        yy = _index(y)
+        return _index(x) + 8 * yy
+
+    # ---------------------------------------------------------------- own / hostile squares of a piece
+    def _empty_mask(self):
+        occ = self._black | self._white
+        for sq in self._other:
+            occ |= 1 << sq
+        return ~occ & _M64
+
+    def _masks(self, piece):
+        """(own, hostile): the squares holding `piece` and hostile(piece) (board.py:155-159)."""
+        hostile = self._white if piece == Black else self._black
+        if piece == Black:
+            own = self._black
+        elif piece == White:
+            own = self._white
+        elif piece == Empty:
+            own = self._empty_mask()
+        else:
+            own = 0
+        for sq, v in self._other.items():
+            if v == piece:
+                own |= 1 << sq
+        return own, hostile
+
+    def _fast(self, piece):
+        """The board-of-three-values path (oth_legal / oth_step) applies."""
+        return not self._other
 
     # ---------------------------------------------------------------- GPU-backed rules
     def _result(self):
@@ -160,12 +335,22 @@ class Board:
         return self._cache[k]
 
     def _legal(self, piece):
-        if piece not in (Black, White):
-            return 0
-        k = ("legal", self._black, self._white, piece)
-        if k not in self._cache:
-            self._cache[k] = _device().legal(self._black, self._white, piece)
-        return self._cache[k]
+        code = _side_code(piece)
+        if self._fast(piece):
+            k = ("legal", self._black, self._white, code)
+            if k not in self._cache:
+                self._cache[k] = _device().legal(self._black, self._white, code)
+            return self._cache[k]
+        # a board holding other values: every square's 8 rays through oth_hands
+        own, hostile = self._masks(piece)
+        rows = [(sq % 8, sq // 8, dx, dy) for sq in range(64) for (dx, dy) in DIRECS]
+        runs = _device().hands(own, hostile, rows)
+        empty = self._empty_mask()
+        m = 0
+        for sq in range(64):
+            if empty >> sq & 1 and any(runs[8 * sq:8 * sq + 8]):
+                m |= 1 << sq
+        return m
 
     def count_over_board(self, fun):  # board.py:29-35
         return sum(1 for y in range(8) for x in range(8) if fun(self.get(x, y)))
@@ -178,7 +363,7 @@ class Board:
 
     def n_empty(self):  # board.py:43-44
         nb, nw, _ = self._result()
-        return 64 - nb - nw
+        return 64 - nb - nw - len(self._other)
 
     def puttables(self, piece):  # board.py:46-52 (row-major == LSB-first)
         m = self._legal(piece)
@@ -190,32 +375,30 @@ class Board:
         return out
 
     def n_puttable_for(self, piece):  # board.py:54-55
-        return bin(self._legal(piece)).count("1")
+        return _popcount(self._legal(piece))
 
     def is_game_over(self):  # board.py:57-58
-        return self._result()[2]
+        if self._fast(None):
+            return self._result()[2]
+        return self.n_puttable_for(Black) == 0 and self.n_puttable_for(White) == 0
+
+    def _runs(self, piece, x, y, direcs):
+        own, hostile = self._masks(piece)
+        return _device().hands(own, hostile, [(_coord(x), _coord(y), _coord(d[0]), _coord(d[1])) for d in direcs])
 
     def is_puttable_at(self, piece, x, y):  # board.py:141-149
-        _check_xy(x, y)
-        return bool(self._legal(piece) >> (x + 8 * y) & 1)
+        if self.get(x, y) != Empty:
+            return False
+        if self._fast(piece) and 0 <= x < 8 and 0 <= y < 8:
+            return bool(self._legal(piece) >> (x + 8 * y) & 1)
+        return sum(self._runs(piece, x, y, DIRECS)) > 0
 
     def hands_for_direc(self, direc, piece, x, y):  # board.py:124-139
-        """Discs captured along one ray from (x, y), as [(piece, nx, ny), ...].
-        The ray scan ignores what stands on (x, y) itself, so the flip mask is
-        taken from the GPU step on the board with the origin square cleared."""
-        _check_xy(x, y)
-        if piece not in (Black, White):
-            raise ValueError("piece must be Black or White")
-        bit = 1 << (x + 8 * y)
-        _, _, fl, _ = _device().step(self._black & ~bit, self._white & ~bit, piece, x + 8 * y)
-        dx, dy = direc
-        ret = []
-        for i in range(1, 9):
-            nx, ny = x + i * dx, y + i * dy
-            if not (0 <= nx < 8 and 0 <= ny < 8) or not fl >> (nx + 8 * ny) & 1:
-                break
-            ret.append((piece, nx, ny))
-        return ret
+        """[(piece, nx, ny), ...] captured along `direc` from (x, y): the run
+        length from oth_hands, the squares are its first steps."""
+        dx, dy = direc[0], direc[1]
+        k = self._runs(piece, x, y, [(dx, dy)])[0]
+        return [(piece, x + i * dx, y + i * dy) for i in range(1, k + 1)]
 
     def set_hands(self, hands):  # board.py:151-153
         for (piece, x, y) in hands:
@@ -224,21 +407,47 @@ class Board:
     def hostile(self, piece):  # board.py:155-159
         return White if piece == Black else Black
 
-    def put(self, piece, x, y):  # board.py:161-174 — flips, no turn change
-        _check_xy(x, y)
-        if piece not in (Black, White):
-            raise ValueError("piece must be Black or White")
-        bl, wh, _, r = _device().step(self._black, self._white, piece, x + 8 * y)
-        if r <= 0:
+    def put(self, piece, x, y):  # board.py:161-174 -- flips, no turn change
+        if self.get(x, y) != Empty:
             return 0
-        self._set_bits(bl, wh)
-        return r
+        if self._fast(piece) and 0 <= x < 8 and 0 <= y < 8:
+            bl, wh, _, r = _device().step(self._black, self._white, _side_code(piece), x + 8 * y)
+            if r <= 0:
+                return 0
+            self._set_bits(bl, wh)
+            return r
+        # an off-board origin or a board holding other values: direction by
+        # direction as board.py does, the runs from oth_hands.  The rays are
+        # disjoint, but from an off-board origin the square set(piece, x, y)
+        # writes (board[y][x], wrapped) can lie on a later ray, so the rays
+        # after a placement are scanned again on the updated board.
+        count = 0
+        runs = self._runs(piece, x, y, DIRECS)
+        for d, (dx, dy) in enumerate(DIRECS):
+            k = runs[d]
+            if k:
+                for i in range(1, k + 1):
+                    self.set(piece, x + i * dx, y + i * dy)  # set_hands
+                count += k
+                self.set(piece, x, y)
+                if d < 7:
+                    runs[d + 1:] = self._runs(piece, x, y, DIRECS[d + 1:])
+        return count
 
     def put_s(self, stri):  # board.py:192-209
         code = codec.move_code(stri)  # raises IndexError for 'a9' like board.py:162
-        bl, wh, _, r = _device().step(self._black, self._white, self.turn, code)
+        if self._fast(self.turn):
+            bl, wh, _, r = _device().step(self._black, self._white, _side_code(self.turn), code)
+            if r >= 0:
+                self._set_bits(bl, wh)
+        elif code == codec.PASS:
+            r = 0
+        elif code < 64:
+            r = self.put(self.turn, code % 8, code // 8)
+            r = -1 if r == 0 else r
+        else:
+            r = -1
         if r >= 0:
-            self._set_bits(bl, wh)
             self.nturn += 1
             self.turn = White if self.turn == Black else Black
         return r
@@ -248,14 +457,23 @@ class Board:
         return "Black" if color == Black else "White" if color == White else "None"
 
     def mask_count(self, color, mask):  # board.py:74-81
-        bb = self._black if color == Black else self._white if color == White else \
-            ~(self._black | self._white) & ((1 << 64) - 1)
-        return bin(bb & mask & ((1 << 64) - 1)).count("1")
+        if color == Black:
+            bb = self._black
+        elif color == White:
+            bb = self._white
+        elif color == Empty:
+            bb = self._empty_mask()
+        else:
+            bb = 0
+        for sq, v in self._other.items():
+            if v == color:
+                bb |= 1 << sq
+        return _popcount(bb & mask)
 
     @classmethod
     def show_mask(cls, mask):  # board.py:83-92
         q = cls()
-        q._set_bits(mask & ((1 << 64) - 1), 0)
+        q._set_bits(mask & _M64, 0)
         print(q)
 
     def __str__(self):  # board.py:94-122
@@ -300,7 +518,12 @@ class Board:
         return codec.turn_from_string(turn_string)
 
     def deserialize(self, board_str, turn_str, nturn):  # board.py:253-262
-        self._set_bits(*codec.deserialize_board(board_str, self._black, self._white))
+        # cell i sets square (i % 8, i // 8); a 65th cell raises IndexError
+        # after the first 64 were set, as board.py's set(cell, 0, 8) does
+        for i, s in enumerate(board_str):
+            if i >= 64:
+                raise IndexError("list index out of range")
+            self._set_cell(i, codec.turn_from_string(s))
         self.turn = codec.turn_from_string(turn_str)
         self.nturn = nturn
 

@@ -220,17 +220,69 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(u64* __restrict__ boards,
     if (nturn) nturn[i] = 0;
 }
 
+// ---------------------------------------------------------------------------
+// Any side to move.  board.py's turn is Black or White in play, but Empty is
+// reachable through deserialize with a side string other than 'O'/'X'
+// (turn_from_string, board.py:245-251), and put/puttables take any piece.
+// For a piece p the scan of hands_for_direc (board.py:124-139) collects
+// squares holding hostile(p) (White for Black, else Black: 155-159) up to a
+// square holding p.  So:
+//   p = Black / White : the usual rule;
+//   p = Empty (0)     : own squares = the empty squares, opponent = Black; a
+//                       run of Black discs ended by an empty square is
+//                       "flipped" to Empty, the origin stays Empty;
+//   p >= 3            : no square holds p, nothing is ever flanked.
+// put_s then toggles the turn to White if it was Black, else to Black (205-208).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 legal_any(u64 bl, u64 wh, u32 t) {
+    if (t == OTH_BLACK) return moves(bl, wh);
+    if (t == OTH_WHITE) return moves(wh, bl);
+    if (t == 0) return moves_empty_side(bl, wh);
+    return 0ull;
+}
+
+struct StepOut {
+    u64 bl, wh, flips;
+    u32 t;
+    int ret;
+};
+// put_s (board.py:192-209) on an integer move code for any side code t
+__device__ __forceinline__ StepOut put_s_any(u64 bl, u64 wh, u32 t, u32 c) {
+    const u64 occ = bl | wh;
+    const bool black = t == OTH_BLACK, white = t == OTH_WHITE;
+    const u64 own = black ? bl : (white ? wh : (t == 0 ? ~occ : 0ull));
+    const u64 opp = black ? wh : bl;
+    StepOut o{bl, wh, 0ull, t, -1};
+    if (c == OTH_PASS) {
+        o.ret = 0;
+    } else if (c < 64 && !(occ >> c & 1ull)) {
+        const u64 f = flips_carry(c, own, opp);  // exact for any own/opp pair (bitboard.hpp)
+        if (f) {
+            const u64 mv = 1ull << c;
+            o.ret = __popcll(f);
+            o.flips = f;
+            if (black) {
+                o.bl = or3(bl, f, mv);
+                o.wh = andn(wh, f);
+            } else if (white) {
+                o.wh = or3(wh, f, mv);
+                o.bl = andn(bl, f);
+            } else {
+                o.bl = andn(bl, f);  // set_hands / set with piece Empty
+            }
+        }
+    }
+    if (o.ret >= 0) o.t = black ? OTH_WHITE : OTH_BLACK;
+    return o;
+}
+
 __global__ __launch_bounds__(kBlock) void legal_kernel(const u64* __restrict__ boards,
                                                        const uint8_t* __restrict__ turn, u64* __restrict__ legal,
                                                        int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards)[i];
-    const u32 t = turn[i];
-    u64 m = 0;
-    if (t == OTH_BLACK) m = moves(b.x, b.y);
-    else if (t == OTH_WHITE) m = moves(b.y, b.x);
-    legal[i] = m;
+    legal[i] = legal_any(b.x, b.y, turn[i]);
 }
 
 // one board of the step (board.py:192-209 semantics, see include/othello.h)
@@ -238,13 +290,13 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
                                            u64* __restrict__ flips_out,
                                            u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
                                            uint8_t* __restrict__ nturn) {
-    const bool valid_turn = (t == OTH_BLACK) | (t == OTH_WHITE);
-    const bool black = t == OTH_BLACK;
-    u64 P = black ? b.x : b.y;
-    u64 O = black ? b.y : b.x;
-    u64 f = 0;
+    u64 nb, nw, f = 0, lg = 0;
+    u32 t_out;
     int r = -1;
-    if (valid_turn) {
+    if (t == OTH_BLACK || t == OTH_WHITE) {
+        const bool black = t == OTH_BLACK;
+        u64 P = black ? b.x : b.y;
+        u64 O = black ? b.y : b.x;
         if (mvc == OTH_PASS) {
             r = 0;
         } else if (mvc < 64) {
@@ -258,25 +310,32 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
                 }
             }
         }
+        const bool moved = r >= 0;
+        t_out = moved ? (t ^ 3u) : t;
+        // one analysis of whichever side moves next (select the operands, not
+        // the results): O if the turn toggled
+        if (legal_next) {
+            const u64 nP = moved ? O : P, nO = moved ? P : O;
+            lg = moves(nP, nO);
+        }
+        nb = black ? P : O;
+        nw = black ? O : P;
+    } else {
+        // side to move Empty (or no colour at all): rare, off the fast path
+        const StepOut o = put_s_any(b.x, b.y, t, mvc);
+        nb = o.bl;
+        nw = o.wh;
+        f = o.flips;
+        r = o.ret;
+        t_out = o.t;
+        if (legal_next) lg = legal_any(nb, nw, t_out);
     }
-    const bool moved = r >= 0;
-    const u32 t_out = moved ? (t ^ 3u) : t;
-    // mover after the step: O if the turn toggled
-    if (legal_next) {
-        // one analysis of whichever side moves next (select the operands, not the results)
-        const u64 nP = moved ? O : P, nO = moved ? P : O;
-        legal_next[i] = valid_turn ? moves(nP, nO) : 0ull;
-    }
-    if (boards_out) {
-        // (an invalid turn leaves P = b.y, O = b.x untouched and black false, so
-        // this already writes the input board back)
-        const u64 nb = black ? P : O, nw = black ? O : P;
-        reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(nb, nw);
-    }
+    if (legal_next) legal_next[i] = lg;
+    if (boards_out) reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(nb, nw);
     if (turn_out) turn_out[i] = (uint8_t)t_out;
     if (flips_out) flips_out[i] = f;
     if (ret_out) ret_out[i] = (int8_t)r;
-    if (nturn && moved) nturn[i] = (uint8_t)(nturn[i] + 1);
+    if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1);
 }
 
 __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, const uint8_t* turn_in,
@@ -294,6 +353,47 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, cons
     step_board(i, b, t, mvc, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
 }
 
+// hands_for_direc (board.py:124-139) for any origin and any direction: the
+// facade's put / is_puttable_at / hands_for_direc with coordinates Python
+// wraps (board[y][x] with x = -1 is file h) or does not check at all.  The scan
+// runs from the origin as given: step k = 1..8 along (dx, dy); a square
+// holding the hostile piece extends the run, one holding the piece itself
+// ends it (kept), anything else -- an off-board step included -- discards it.
+// So from an off-board origin a ray exists only if its first step lands on
+// the board, and a run of 8 hostile squares is kept without a closing piece
+// (board.py:129's loop ends first).  The returned squares are always those of
+// steps 1..count, so the count is the whole answer.  One thread per
+// (origin, direction), eight steps of two bit tests: the facade's
+// batch-of-one calls, not a throughput path.
+__device__ __forceinline__ bool step_on_board(int64_t x, int64_t d, int k, int64_t& out) {
+    int64_t t;
+    // an overflowing coordinate is far off the board
+    return !__builtin_mul_overflow(d, (int64_t)k, &t) && !__builtin_add_overflow(x, t, &out) && out >= 0 && out < 8;
+}
+__global__ __launch_bounds__(kBlock) void hands_kernel(const u64* __restrict__ own, const u64* __restrict__ hostile,
+                                                       const int64_t* __restrict__ xs, const int64_t* __restrict__ ys,
+                                                       const int64_t* __restrict__ dxs,
+                                                       const int64_t* __restrict__ dys,
+                                                       uint8_t* __restrict__ count, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const u64 mine = own[i], opp = hostile[i];
+    const int64_t x = xs[i], y = ys[i], dx = dxs[i], dy = dys[i];
+    int run = 0;
+    for (int k = 1; k < 9; k++) {
+        int64_t nx, ny;
+        const bool on = step_on_board(x, dx, k, nx) && step_on_board(y, dy, k, ny);
+        const u64 bit = on ? 1ull << (nx + 8 * ny) : 0ull;
+        if (opp & bit) {
+            run = k;  // (a zero direction revisits one square: board.py appends it again)
+        } else {
+            if (!(mine & bit)) run = 0;  // empty / other / off-board: discard
+            break;                       // own piece: keep
+        }
+    }
+    count[i] = (uint8_t)run;
+}
+
 __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ boards, uint8_t* __restrict__ nb,
                                                         uint8_t* __restrict__ nw, int8_t* __restrict__ diff,
                                                         uint8_t* __restrict__ terminal, int64_t n) {
@@ -309,18 +409,19 @@ __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // rollout kernel: persistent waves (grid = resident capacity); each wave
-// dequeues a batch of 64 game ids (ONE returning atomic), plays the 64 games
-// to terminal in lockstep -- a finished lane is masked off by __ballot until
-// the whole batch is done -- and dequeues again.  The hardware balances the
-// batches; no refill code runs inside the ply loop (measured cheaper than
-// per-lane refill, DESIGN.md §Rollout scheduling).
+// dequeues a batch of 64 game ids (ONE returning atomic on the caller's work
+// word), plays the 64 games to terminal in lockstep -- a finished lane is
+// masked off until the whole batch is done -- and dequeues again.  The
+// hardware balances the batches; no refill code runs inside the ply loop
+// (measured cheaper than per-lane refill, DESIGN.md §Rollout scheduling).
+//
+// The work word is the caller's (include/othello.h): 0 when the launch
+// starts, and 0 again when it ends.  A launch of B batches on W waves makes
+// exactly B + W dequeues (one per batch, one failing dequeue per wave), so the
+// dequeue that draws ticket 64 * (B + W - 1) is the last one of the launch and
+// its wave puts the word back to 0.  No reset runs on the stream, and a graph
+// replay finds the word at 0 like an eager launch does.
 // ---------------------------------------------------------------------------
-constexpr int kWorkSlots = 64;  // concurrent launches supported (distinct streams)
-// captured launches (hipGraph) use their own slots: a replay cannot update the
-// host shadow, so a captured launch records a memset node and starts from 0
-constexpr int kGraphSlots = 64;
-constexpr int kCtrStride = 16;  // u64 words between counters (128 B)
-__device__ unsigned long long g_work[(kWorkSlots + kGraphSlots) * kCtrStride];
 
 struct RolloutArgs {
     const u64* start;
@@ -334,8 +435,8 @@ struct RolloutArgs {
     uint8_t* moves;
     long long* hist;
     int64_t n;
-    unsigned long long* work;  // batch counter slot (monotonic across launches)
-    u64 work_base;             // its value when this launch starts (host-tracked)
+    unsigned long long* work;  // the caller's work word (0 at start, left at 0)
+    u64 last_ticket;           // 64 * (batches + waves - 1): the launch's last dequeue
     EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table
 };
 
@@ -372,7 +473,10 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     for (;;) {
         // ---- dequeue a batch of 64 games (one per lane)
         u64 base = 0;
-        if (lane == 0) base = atomicAdd(a.work, 64ull) - a.work_base;
+        if (lane == 0) {
+            base = atomicAdd(a.work, 64ull);
+            if (base == a.last_ticket) atomicExch(a.work, 0ull);  // every dequeue is done: reset
+        }
         base = __shfl(base, 0);
         if (base >= n) break;  // wave-uniform
 
@@ -630,7 +734,12 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ 
                 ee[k] = (moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0) ? 1 : 0;
                 // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
                 const u32 p = p0 + k;
-                if (p < np && (t == OTH_BLACK || t == OTH_WHITE)) {
+                if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
+                    const StepOut o = put_s_any(bl, wh, t, mv[p]);  // side Empty / none (rare)
+                    bl = o.bl;
+                    wh = o.wh;
+                    t = o.t;
+                } else if (p < np) {
                     const u32 c = mv[p];
                     if (c == OTH_PASS) {
                         t ^= 3u;
@@ -1053,28 +1162,19 @@ inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
 struct Tuning {
     unsigned resident_blocks[3];  // per policy
 };
-std::atomic<unsigned long long> g_slot{0};
-std::atomic<unsigned long long> g_graph_slot{0};
 
 int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
 
-// per-device caches (a process may drive several GPUs); resolved on first use
+// per-device launch geometry (a process may drive several GPUs), resolved on
+// first use; the only state the library keeps, and none of it on the device
 constexpr int kMaxDevices = 64;
 constexpr int kMaxBlocksPerCu = 5;
 struct DeviceState {
     std::atomic<int> ready{0};
     Tuning tuning;
-    unsigned long long* work = nullptr;
-    // Host shadow of each counter slot.  A launch of B batches on W waves
-    // advances its slot by exactly 64 * (B + W) (every batch is one successful
-    // dequeue, every wave ends on one failing dequeue), so the next launch on
-    // the slot knows its starting value without a reset on the stream.  A slot
-    // whose launch failed is reset with a memset before its next use.
-    std::atomic<unsigned long long> slot_base[kWorkSlots];
-    std::atomic<bool> slot_dirty[kWorkSlots];
 };
 DeviceState g_dev[kMaxDevices];
 std::mutex g_dev_mu;
@@ -1102,9 +1202,6 @@ DeviceState* device_state() {
             per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu);
             d.tuning.resident_blocks[p] = (unsigned)(cus * per_cu);
         }
-        void* q = nullptr;
-        if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_work)) != hipSuccess || !q) return nullptr;
-        d.work = reinterpret_cast<unsigned long long*>(q);
         d.ready.store(1, std::memory_order_release);
     }
     return &d;
@@ -1145,6 +1242,14 @@ int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* m
     return launched();
 }
 
+int oth_hands(const uint64_t* own, const uint64_t* hostile, const int64_t* x, const int64_t* y, const int64_t* dx,
+              const int64_t* dy, uint8_t* count, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!own || !hostile || !x || !y || !dx || !dy || !count))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    hands_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(own, hostile, x, y, dx, dy, count, n);
+    return launched();
+}
+
 int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_t* diff, uint8_t* terminal,
                int64_t n, void* stream) {
     if (n < 0 || (n > 0 && !boards)) return OTH_EINVAL;
@@ -1156,7 +1261,7 @@ int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_
 namespace {
 int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, const int8_t* w_black, const int8_t* w_white, uint64_t* final_boards, int8_t* diff,
-                   uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
+                   uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream) {
     RolloutArgs a;
     a.start = start;
     a.start_turn = start_turn;
@@ -1178,31 +1283,8 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     const Tuning& t = ds->tuning;
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
-    DeviceState& dsm = *ds;
-    int slot = -1;
-    if (cap == hipStreamCaptureStatusActive) {
-        // a graph node: every replay resets its own slot first
-        const int gs = (int)(g_graph_slot.fetch_add(1, std::memory_order_relaxed) % kGraphSlots);
-        a.work = ds->work + (size_t)(kWorkSlots + gs) * kCtrStride;
-        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
-        if (e != hipSuccess) return status(e);
-        a.work_base = 0;
-    } else {
-        slot = (int)(g_slot.fetch_add(1, std::memory_order_relaxed) % kWorkSlots);
-        a.work = ds->work + (size_t)slot * kCtrStride;
-        if (dsm.slot_dirty[slot].exchange(false)) {
-            hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned long long), (hipStream_t)stream);
-            if (e != hipSuccess) {
-                dsm.slot_dirty[slot].store(true);
-                return status(e);
-            }
-            dsm.slot_base[slot].store(0);
-        }
-        const u64 advance = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64));
-        a.work_base = dsm.slot_base[slot].fetch_add(advance);
-    }
+    a.work = reinterpret_cast<unsigned long long*>(work);
+    a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
     hipStream_t st = (hipStream_t)stream;
     if (policy == OTH_POLICY_EVAL) {
         if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
@@ -1214,37 +1296,36 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
         if (moves) rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
-    const int rc = launched();
-    if (rc != OTH_OK && slot >= 0) dsm.slot_dirty[slot].store(true);  // counter state unknown: reset before reuse
-    return rc;
+    return launched();
 }
 }  // namespace
 
 int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                 int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist,
-                int64_t n, void* stream) {
-    if (n < 0 || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
+                uint64_t* work, int64_t n, void* stream) {
+    if (n < 0 || !work || (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY)) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return rollout_launch(start, start_turn, seed, game_id0, policy, n_random, nullptr, nullptr, final_boards, diff,
-                          plies, moves, hist, n, stream);
+                          plies, moves, hist, work, n, stream);
 }
 
 int oth_rollout_eval(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                      int n_random, const int8_t* weights, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
-                     uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
-    if (n < 0 || !weights) return OTH_EINVAL;
+                     uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream) {
+    if (n < 0 || !weights || !work) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights, weights, final_boards,
-                          diff, plies, moves, hist, n, stream);
+                          diff, plies, moves, hist, work, n, stream);
 }
 
 int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
                       int n_random, const int8_t* weights_black, const int8_t* weights_white, uint64_t* final_boards,
-                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, int64_t n, void* stream) {
-    if (n < 0 || !weights_black || !weights_white) return OTH_EINVAL;
+                      int8_t* diff, uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n,
+                      void* stream) {
+    if (n < 0 || !weights_black || !weights_white || !work) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     return rollout_launch(start, start_turn, seed, game_id0, OTH_POLICY_EVAL, n_random, weights_black, weights_white,
-                          final_boards, diff, plies, moves, hist, n, stream);
+                          final_boards, diff, plies, moves, hist, work, n, stream);
 }
 
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,

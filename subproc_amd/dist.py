@@ -54,8 +54,21 @@ def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None,
     if end > begin:
         rollout_fn(end - begin, seed, game_id_base + begin, policy, n_random, hist)
     if world > 1:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        reduce_histogram(hist, group)
     return hist, end - begin
+
+
+def reduce_histogram(hist, group=None):
+    """The one collective: all_reduce(SUM) of the int64[133] histogram, in
+    place.  RCCL ("nccl") reduces the device tensor where it lies; a gloo
+    group (CPU tests, or ranks sharing one GPU) reduces a host copy."""
+    if hist.is_cuda and dist.get_backend(group) == "gloo":
+        h = hist.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        hist.copy_(h)
+    else:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    return hist
 
 
 def hist_summary(hist):

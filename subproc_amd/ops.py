@@ -12,6 +12,7 @@ Reference mapping (board.py line numbers):
   legal   -> Board.puttables           46-52   (n_puttable_for = popcount)
   step    -> Board.put_s / put         161-209
   result  -> n_black / n_white / is_game_over 37-58 + game_runner.py:194-199
+  hands   -> Board.hands_for_direc     124-139 (any origin, all 8 directions)
   rollout -> GameRunner.play_a_game loop   game_runner.py:165-201
   evaluate -> linear eval of the learner's counts() features
 """
@@ -22,8 +23,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, POLICY_EVAL, POLICY_GREEDY, POLICY_RANDOM,
-                   POS_STRIDE, check)
+from ._lib import (BLACK, BOOK_LINE, HIST_BINS, MOVES_STRIDE, N_FEATURES, PASS, POLICY_EVAL, POLICY_GREEDY,
+                   POLICY_RANDOM, POS_STRIDE, WHITE, check)
 from .params import DEFAULT_WEIGHTS, as_weights
 
 StepResult = namedtuple("StepResult", "boards turn flips legal_next ret")
@@ -151,9 +152,42 @@ def result(boards):
     return Result(nb, nw, df, te)
 
 
+def hands(own, hostile, x, y, dx, dy):
+    """len(Board.hands_for_direc((dx, dy), piece, x, y)) (board.py:124-139) per
+    item, for any origin and direction (int64: off-board origins included);
+    own[i] / hostile[i] = squares holding the piece / hostile(piece).  The
+    returned squares are (x + k*dx, y + k*dy), k = 1..count: (n,) uint8."""
+    n = own.shape[0]
+    po = _dev(own, "own", torch.int64, (n,))
+    ph = _dev(hostile, "hostile", torch.int64, (n,), own.device)
+    pc = [_dev(v, nm, torch.int64, (n,), own.device) for v, nm in ((x, "x"), (y, "y"), (dx, "dx"), (dy, "dy"))]
+    out = torch.empty(n, dtype=torch.uint8, device=own.device)
+    with torch.cuda.device(own.device):
+        check(_lib.load().oth_hands(po, ph, *pc, out.data_ptr(), n, _stream()), "oth_hands")
+    return out
+
+
+_WORK = {}
+
+
+def work_word(device=None):
+    """The rollout work word of torch's current stream on `device` (one zeroed
+    device uint64 per (device, stream), include/othello.h oth_rollout): a
+    launch finds it at 0 and leaves it at 0, so launches ordered on one stream
+    share it and launches on different streams never do."""
+    d = _device("cuda" if device is None else device)
+    with torch.cuda.device(d):
+        key = (d.index, torch.cuda.current_stream().cuda_stream)
+        w = _WORK.get(key)
+        if w is None:
+            w = torch.zeros(1, dtype=torch.int64, device=d)  # zeroed on this stream, before any launch on it
+            _WORK[key] = w
+    return w
+
+
 def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start_turn=None, record_moves=False,
             hist=None, device="cuda", want_boards=True, want_diff=True, want_plies=True, weights=None,
-            weights_white=None):
+            weights_white=None, work=None):
     """Play n games to terminal on the GPU (one lane per game).
 
     Game i uses the RNG stream of global id game_id0 + i, so results do not
@@ -167,6 +201,9 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     params.DEFAULT_WEIGHTS) after ``n_random`` random plies.  With
     ``weights_white`` the eval policy is a match: Black plays ``weights``,
     White plays ``weights_white`` (oth_rollout_match).
+
+    ``work`` (int64 (1,) device tensor, 0 at the launch) is the launch's batch
+    counter; default: the current stream's :func:`work_word`.
     """
     if policy not in _POLICIES:
         raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
@@ -184,24 +221,30 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     if hist is None:
         hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=d)
     ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
+    if _POLICIES[policy] != POLICY_EVAL and (weights is not None or weights_white is not None):
+        raise ValueError("weights apply to policy 'eval' only")
+    w = work_word(d) if work is None else work
+    pw = _dev(w, "work", torch.int64, (1,), d)
 
     def ptr(t):
         return None if t is None else t.data_ptr()
 
     with torch.cuda.device(d):
+        seed64 = seed & (2**64 - 1)
         if _POLICIES[policy] == POLICY_EVAL and weights_white is not None:
-            check(_lib.load().oth_rollout_match(ps, pst, seed & (2**64 - 1), game_id0, n_random,
-                                                _weights_ptr(weights), _weights_ptr(weights_white), ptr(fb), ptr(df),
-                                                ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout_match")
+            rc, what = _lib.load().oth_rollout_match(ps, pst, seed64, game_id0, n_random, _weights_ptr(weights),
+                                                     _weights_ptr(weights_white), ptr(fb), ptr(df), ptr(pl), ptr(mv),
+                                                     ph, pw, n, _stream()), "oth_rollout_match"
         elif _POLICIES[policy] == POLICY_EVAL:
-            check(_lib.load().oth_rollout_eval(ps, pst, seed & (2**64 - 1), game_id0, n_random, _weights_ptr(weights),
-                                               ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()),
-                  "oth_rollout_eval")
+            rc, what = _lib.load().oth_rollout_eval(ps, pst, seed64, game_id0, n_random, _weights_ptr(weights),
+                                                    ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, pw, n,
+                                                    _stream()), "oth_rollout_eval"
         else:
-            if weights is not None or weights_white is not None:
-                raise ValueError("weights apply to policy 'eval' only")
-            check(_lib.load().oth_rollout(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy], n_random,
-                                          ptr(fb), ptr(df), ptr(pl), ptr(mv), ph, n, _stream()), "oth_rollout")
+            rc, what = _lib.load().oth_rollout(ps, pst, seed64, game_id0, _POLICIES[policy], n_random, ptr(fb),
+                                               ptr(df), ptr(pl), ptr(mv), ph, pw, n, _stream()), "oth_rollout"
+        if rc != _lib.OTH_OK:
+            w.zero_()  # a failed launch leaves the counter unknown (include/othello.h)
+        check(rc, what)
     return RolloutResult(fb, df, pl, mv, hist)
 
 
@@ -290,6 +333,6 @@ def from_numpy_u64(a, device="cuda"):
     return torch.from_numpy(a.view(np.int64).copy()).to(device)
 
 
-__all__ = ["reset", "legal", "step", "result", "rollout", "sample_midgame", "replay", "book_text", "features",
-           "to_numpy_u64", "from_numpy_u64",
-           "StepResult", "Result", "RolloutResult", "Positions", "BLACK", "WHITE", "PASS", "HIST_BINS"]
+__all__ = ["reset", "legal", "step", "result", "hands", "rollout", "work_word", "sample_midgame", "replay",
+           "book_text", "features", "evaluate", "to_numpy_u64", "from_numpy_u64",
+           "StepResult", "Result", "RolloutResult", "Positions", "Replay", "BLACK", "WHITE", "PASS", "HIST_BINS"]

@@ -322,10 +322,165 @@ def u64(a):
     return np.array(a, dtype=np.uint64)
 
 
+# ----------------------------------------------------------------------------
+# board_api: the inputs board.py accepts beyond Black/White play (round 2)
+# ----------------------------------------------------------------------------
+OTHER = 3  # a piece / side value equal to none of Empty, Black, White
+API_PIECES = (Empty, Black, White, OTHER)
+API_XY = tuple(range(-8, 8))       # what board[y][x] accepts (negatives wrap)
+SCAN_XY = tuple(range(-3, 11))     # hands_for_direc takes any origin
+SCAN_DIRECS = list(RB["DIRECS"]) + [(0, 0), (2, 1), (-1, 3)]
+
+
+def api_boards(pos):
+    """Positions for the piece/coordinate fixtures: reachable mid-game boards
+    plus boards built to hit the unusual branches -- full rows/diagonals (a
+    run of 8 hostile squares from an off-board origin), the wrapped origin on
+    a later ray of put, and Black runs ending on empty squares."""
+    out = [(p[0], p[1]) for p in pos[:24]]
+    out += [
+        (0, 0xFF),                                   # row 1 all White
+        (0xFF, 0),                                   # row 1 all Black
+        (0x8040201008040201, 0),                     # a1-h8 diagonal Black
+        (0, 0x0102040810204080),                     # h1-a8 diagonal White
+        (0x0000000000020000, 0x0000007F01000000),    # put(Black, -1, 4): RU, then R through the wrapped h5
+        (0x0000007F00000000, 0x0000000000080000),    # Black row e..: runs ending on empties
+        (0x00FF00000000FF00, 0x0000FF0000FF0000),
+        (0x0101010101010101, 0x8080808080808080),    # files a / h full
+    ]
+    return out
+
+
+def api_record(args):
+    """For one board: put / is_puttable_at for every piece and (x, y) in
+    -8..7, puttables for every piece, hands_for_direc lengths for SCAN_XY x
+    SCAN_DIRECS, through board.py itself."""
+    bl, wh = args
+    b0 = from_bits(bl, wh, Black)
+    n_xy = len(API_XY)
+    put_ret = np.zeros((len(API_PIECES), n_xy, n_xy), np.int8)
+    put_black = np.zeros((len(API_PIECES), n_xy, n_xy), np.uint64)
+    put_white = np.zeros((len(API_PIECES), n_xy, n_xy), np.uint64)
+    puttable = np.zeros((len(API_PIECES), n_xy, n_xy), np.uint8)
+    legal = np.zeros(len(API_PIECES), np.uint64)
+    hands = np.zeros((len(API_PIECES), len(SCAN_DIRECS), len(SCAN_XY), len(SCAN_XY)), np.uint8)
+    for pi, piece in enumerate(API_PIECES):
+        legal[pi] = legal_bits(b0, piece)
+        for iy, y in enumerate(API_XY):
+            for ix, x in enumerate(API_XY):
+                puttable[pi, iy, ix] = b0.is_puttable_at(piece, x, y)
+                b = clone(b0)
+                put_ret[pi, iy, ix] = b.put(piece, x, y)
+                assert all(c in (Empty, Black, White) for row in b.board for c in row)
+                put_black[pi, iy, ix], put_white[pi, iy, ix] = to_bits(b)
+        for di, d in enumerate(SCAN_DIRECS):
+            for iy, y in enumerate(SCAN_XY):
+                for ix, x in enumerate(SCAN_XY):
+                    hs = b0.hands_for_direc(d, piece, x, y)
+                    assert hs == [(piece, x + i * d[0], y + i * d[1]) for i in range(1, len(hs) + 1)]
+                    hands[pi, di, iy, ix] = len(hs)
+    return legal, puttable, put_ret, put_black, put_white, hands
+
+
+def side_steps(args):
+    """Every code 0..64 through put_s with the side to move `turn` (Empty via
+    deserialize(..., '-', n), or a value no square holds), board.py:192-209."""
+    bl, wh, turn = args
+    b0 = from_bits(bl, wh, Black)
+    if turn == Empty:
+        b0.deserialize(b0.serialize_board(), "-", 7)
+        assert b0.turn == Empty
+    else:
+        b0.turn, b0.nturn = turn, 7
+    out = []
+    for code in range(65):
+        b = clone(b0)
+        r = b.put_s(code_to_str(b, code))
+        nb, nw = to_bits(b)
+        out.append((r, nb, nw, b.turn, b.nturn, legal_bits(b, b.turn)))
+    return legal_bits(b0, b0.turn), out
+
+
+def board_api_fixtures(pos, pool):
+    boards = api_boards(pos)
+    res = pool.map(api_record, boards, chunksize=1)
+    np.savez_compressed(
+        os.path.join(OUT, "board_api.npz"),
+        black=u64([b[0] for b in boards]), white=u64([b[1] for b in boards]),
+        pieces=np.array(API_PIECES, np.uint8), xy=np.array(API_XY, np.int64), scan_xy=np.array(SCAN_XY, np.int64),
+        scan_direcs=np.array(SCAN_DIRECS, np.int64),
+        legal=np.stack([r[0] for r in res]), puttable=np.stack([r[1] for r in res]),
+        put_ret=np.stack([r[2] for r in res]), put_black=np.stack([r[3] for r in res]),
+        put_white=np.stack([r[4] for r in res]), hands=np.stack([r[5] for r in res]))
+    # side to move Empty / other: every code
+    cases = [(p[0], p[1], t) for t in (Empty, OTHER) for p in pos[:256]]
+    res = pool.map(side_steps, cases, chunksize=8)
+    np.savez_compressed(
+        os.path.join(OUT, "side_steps.npz"),
+        black=u64([c[0] for c in cases]), white=u64([c[1] for c in cases]),
+        turn=np.array([c[2] for c in cases], np.uint8), legal=u64([r[0] for r in res]),
+        ret=np.array([[o[0] for o in r[1]] for r in res], np.int8),
+        next_black=u64([[o[1] for o in r[1]] for r in res]), next_white=u64([[o[2] for o in r[1]] for r in res]),
+        next_turn=np.array([[o[3] for o in r[1]] for r in res], np.uint8),
+        next_nturn=np.array([[o[4] for o in r[1]] for r in res], np.uint8),
+        next_legal=u64([[o[5] for o in r[1]] for r in res]))
+    # the live board list, other-valued cells and deserialize edge cases (JSON)
+    recs = []
+    for name, ops_ in [
+        ("write_through", [("board", 2, 3, White), ("board", 4, 4, Empty), ("set", Black, -1, -1),
+                           ("set", White, 0, -8)]),
+        ("other_values", [("set", 5, 2, 3), ("set", 5, 5, 4), ("set", "x", -3, -2)]),
+        ("other_blocks_run", [("set", 7, 5, 3), ("board", 3, 5, 7)]),
+    ]:
+        b = Board()
+        for op in ops_:
+            if op[0] == "board":
+                b.board[op[1]][op[2]] = op[3]
+            else:
+                b.set(op[1], op[2], op[3])
+        rec = {"name": name, "ops": [list(o) for o in ops_],
+               "cells": [[c if isinstance(c, int) else str(c) for c in row] for row in b.board],
+               "n_black": b.n_black(), "n_white": b.n_white(), "n_empty": b.n_empty(),
+               "is_game_over": b.is_game_over(), "serialize_str": b.serialize_str(), "str": str(b),
+               "puttables": {str(p): b.puttables(p) for p in (Empty, Black, White, 5, 7)},
+               "mask_count": {str(p): b.mask_count(p, 0x00FFFF0000FFFF00) for p in (Empty, Black, White, 5, 7)},
+               "get": [b.get(x, y) if isinstance(b.get(x, y), int) else str(b.get(x, y))
+                       for (x, y) in ((-1, -1), (3, 2), (-5, -6), (2, 3))],
+               "put_s": []}
+        for code in range(65):
+            c = clone(b)
+            r = c.put_s(code_to_str(c, code))
+            rec["put_s"].append({"code": code, "ret": r, "turn": c.turn,
+                                 "cells": [[v if isinstance(v, int) else str(v) for v in row] for row in c.board]})
+        rec["put"] = []
+        for piece in (Empty, Black, White, 5, 7):
+            for (x, y) in ((2, 2), (-1, 4), (3, 3), (5, 2), (0, -1), (4, 2)):
+                c = clone(b)
+                r = c.put(piece, x, y)
+                rec["put"].append({"piece": piece, "x": x, "y": y, "ret": r,
+                                   "cells": [[v if isinstance(v, int) else str(v) for v in row] for row in c.board]})
+        recs.append(rec)
+    dz = []
+    for bstr, tstr in (("O" * 70, "X"), ("-" * 10, "O"), ("XO" * 32, "?")):
+        b = Board()
+        try:
+            b.deserialize(bstr, tstr, 3)
+            raised = False
+        except IndexError:
+            raised = True
+        dz.append({"board": bstr, "turn_str": tstr, "raises": raised, "cells": [list(r) for r in b.board],
+                   "turn": b.turn, "nturn": b.nturn})
+    json.dump({"boards": recs, "deserialize": dz}, open(os.path.join(OUT, "board_api.json"), "w"))
+
+
 def main():
     pool = mp.Pool(8)
     init = Board()
     ib, iw = to_bits(init)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "board_api":
+        board_api_fixtures(random_positions(1024, 20240601), pool)
+        print("board_api fixtures written to", OUT)
+        return
 
     # ---------------------------------------------------------------- opening
     opening = {"black": hex(ib), "white": hex(iw), "turn": init.turn, "nturn": init.nturn,
@@ -405,6 +560,8 @@ def main():
         next_nturn=np.array([[o[4] for o in r[1]] for r in res], np.uint8),
         next_legal=u64([[o[5] for o in r[1]] for r in res]),
     )
+
+    board_api_fixtures(pos, pool)
 
     # ---------------------------------------------------------------- rollouts
     def rollouts(name, seed, g0, n, policy, n_random, starts=None, weights=None, weights_white=None):

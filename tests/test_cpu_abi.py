@@ -18,6 +18,9 @@ from subproc_amd import _lib
 P = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
 
 
+WORK = np.zeros(1, np.uint64)  # the rollouts' work word (unused by the host build, but required)
+
+
 def lib():
     return oracle.cpu_abi()
 
@@ -81,14 +84,14 @@ def test_rollout_fixtures(name):
         w = np.ascontiguousarray(z["weights"].reshape(-1), np.int8)
         ww = np.ascontiguousarray(z["weights_white"].reshape(-1), np.int8)
         rc = lib().oth_rollout_match(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["n_random"]), P(w),
-                                     P(ww), P(fb), P(df), P(pl), P(mv), P(hist), n, None)
+                                     P(ww), P(fb), P(df), P(pl), P(mv), P(hist), P(WORK), n, None)
     elif int(z["policy"]) == 2:
         w = np.ascontiguousarray(z["weights"].reshape(-1), np.int8)
         rc = lib().oth_rollout_eval(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["n_random"]), P(w),
-                                    P(fb), P(df), P(pl), P(mv), P(hist), n, None)
+                                    P(fb), P(df), P(pl), P(mv), P(hist), P(WORK), n, None)
     else:
         rc = lib().oth_rollout(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["policy"]),
-                               int(z["n_random"]), P(fb), P(df), P(pl), P(mv), P(hist), n, None)
+                               int(z["n_random"]), P(fb), P(df), P(pl), P(mv), P(hist), P(WORK), n, None)
     assert rc == 0
     np.testing.assert_array_equal(mv, z["moves"])
     np.testing.assert_array_equal(fb[:, 0], z["final_black"])
@@ -139,6 +142,8 @@ def test_sample_midgame_fixture_and_einval():
     assert lib().oth_sample_midgame(int(z["seed"]), 0, P(b), P(t), P(nt), P(m), n, None) == 0
     np.testing.assert_array_equal(b[:, 0], z["black"])
     np.testing.assert_array_equal(m, z["move"])
-    assert lib().oth_rollout(None, None, 1, 0, 7, 0, None, None, None, None, None, 4, None) == _lib.OTH_EINVAL
+    assert lib().oth_rollout(None, None, 1, 0, 7, 0, None, None, None, None, None, P(WORK), 4, None) == _lib.OTH_EINVAL
+    # the work word is required (include/othello.h)
+    assert lib().oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, None, 4, None) == _lib.OTH_EINVAL
     assert lib().oth_step(None, None, None, None, None, None, None, None, None, 3, None) == _lib.OTH_EINVAL
     assert lib().oth_eval(None, None, None, None, 0, None) == _lib.OTH_EINVAL

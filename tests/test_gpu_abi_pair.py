@@ -44,6 +44,11 @@ def both(name, *args):
     torch.cuda.synchronize()
 
 
+def work():
+    """A rollout work word for both builds (include/othello.h: 0 at the call)."""
+    return Buf(np.zeros(1, np.uint64))
+
+
 def same(*bufs):
     for b in bufs:
         np.testing.assert_array_equal(b.device_as_host(), b.h)
@@ -180,20 +185,22 @@ def test_rollout_pair(policy):
     b, t, _, _ = positions(n, 3)
     outs = [Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.int8)), Buf(np.zeros(n, np.uint8)),
             Buf(np.zeros((n, _lib.MOVES_STRIDE), np.uint8)), Buf(np.zeros(_lib.HIST_BINS, np.int64))]
+    wk = work()
     if policy == 2:
         w = (ctypes.c_int8 * 36)(*np.random.default_rng(1).integers(-127, 128, 36).tolist())
-        both("oth_rollout_eval", None, None, 99, 1 << 30, 10, w, *outs, n)
-        both("oth_rollout_eval", b, t, 98, 5, 0, w, *outs, n)  # from mid-game starts, hist accumulates
+        both("oth_rollout_eval", None, None, 99, 1 << 30, 10, w, *outs, wk, n)
+        both("oth_rollout_eval", b, t, 98, 5, 0, w, *outs, wk, n)  # from mid-game starts, hist accumulates
     else:
-        both("oth_rollout", None, None, 99, 1 << 30, policy, 10, *outs, n)
-        both("oth_rollout", b, t, 98, 5, policy, 0, *outs, n)
+        both("oth_rollout", None, None, 99, 1 << 30, policy, 10, *outs, wk, n)
+        both("oth_rollout", b, t, 98, 5, policy, 0, *outs, wk, n)
     same(*outs)
+    assert int(wk.d.item()) == 0  # every launch leaves its work word at 0
 
 
 def test_books_features_eval_pair():
     n = 512
     outs = [None, None, Buf(np.zeros(n, np.uint8)), Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8)), None]
-    both("oth_rollout", None, None, 5, 0, 0, 0, None, None, outs[2], outs[3], None, n)
+    both("oth_rollout", None, None, 5, 0, 0, 0, None, None, outs[2], outs[3], None, work(), n)
     same(outs[2], outs[3])
     pos = Buf(np.zeros((n, _lib.POS_STRIDE, 2), np.uint64))
     pt, pe = Buf(np.zeros((n, _lib.POS_STRIDE), np.uint8)), Buf(np.zeros((n, _lib.POS_STRIDE), np.uint8))
@@ -219,7 +226,7 @@ def test_td_pair():
     n = 256
     plies = Buf(np.zeros(n, np.uint8))
     moves = Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8))
-    both("oth_rollout", None, None, 21, 0, 1, 4, None, None, plies, moves, None, n)
+    both("oth_rollout", None, None, 21, 0, 1, 4, None, None, plies, moves, None, work(), n)
     same(plies, moves)
     pos = Buf(np.zeros((n, _lib.POS_STRIDE, 2), np.uint64))
     both("oth_replay", None, None, moves, plies, pos, None, None, n)
@@ -259,14 +266,16 @@ def test_empty_null_and_invalid_arguments():
     gpu, cpu = _lib.load(), oracle.cpu_abi()
     st = torch.cuda.current_stream().cuda_stream
     w = (ctypes.c_int8 * 36)()
-    for lib, s in ((gpu, st), (cpu, None)):
+    wk = work()
+    for lib, s, W in ((gpu, st, wk.d.data_ptr()), (cpu, None, HOSTP(wk.h))):
         assert lib.oth_reset(None, None, None, 0, s) == 0
         assert lib.oth_legal(None, None, None, 0, s) == 0
         assert lib.oth_step(None, None, None, None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_result(None, None, None, None, None, 0, s) == 0
-        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, 0, s) == 0
-        assert lib.oth_rollout_eval(None, None, 1, 0, 0, w, None, None, None, None, None, 0, s) == 0
-        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, w, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, W, 0, s) == 0
+        assert lib.oth_rollout_eval(None, None, 1, 0, 0, w, None, None, None, None, None, W, 0, s) == 0
+        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, w, None, None, None, None, None, W, 0, s) == 0
+        assert lib.oth_hands(None, None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_replay(None, None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_book_text(None, None, 0, None, s) == 0
         assert lib.oth_features(None, None, None, 0, s) == 0
@@ -277,10 +286,13 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_sample_midgame(1, 0, None, None, None, None, 0, s) == 0
         E = _lib.OTH_EINVAL
         assert lib.oth_step(None, None, None, None, None, None, None, None, None, 5, s) == E
-        assert lib.oth_rollout(None, None, 1, 0, 3, 0, None, None, None, None, None, 5, s) == E  # bad policy
-        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, -1, s) == E
-        assert lib.oth_rollout_eval(None, None, 1, 0, 0, None, None, None, None, None, None, 5, s) == E
-        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, None, None, None, None, None, None, 5, s) == E
+        assert lib.oth_rollout(None, None, 1, 0, 3, 0, None, None, None, None, None, W, 5, s) == E  # bad policy
+        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, W, -1, s) == E
+        assert lib.oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, None, 5, s) == E  # no work word
+        assert lib.oth_rollout_eval(None, None, 1, 0, 0, None, None, None, None, None, None, W, 5, s) == E
+        assert lib.oth_rollout_eval(None, None, 1, 0, 0, w, None, None, None, None, None, None, 5, s) == E
+        assert lib.oth_rollout_match(None, None, 1, 0, 0, w, None, None, None, None, None, None, W, 5, s) == E
+        assert lib.oth_hands(None, None, None, None, None, None, None, 3, s) == E
         assert lib.oth_eval(None, None, None, None, 0, s) == E
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 3, s) == E
         assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 0, None, 0, s) == E  # long_min < 1
@@ -309,6 +321,6 @@ def test_empty_null_and_invalid_arguments():
     # every rollout output may be NULL: only the histogram is produced
     n = 4096
     hist = Buf(np.zeros(_lib.HIST_BINS, np.int64))
-    both("oth_rollout", None, None, 12, 0, 0, 10, None, None, None, None, hist, n)
+    both("oth_rollout", None, None, 12, 0, 0, 10, None, None, None, None, hist, work(), n)
     same(hist)
     assert int(hist.h[:129].sum()) == n

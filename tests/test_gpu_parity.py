@@ -86,12 +86,20 @@ def test_edges():
             assert int(r.turn[i]) == s["turn"]
 
 
-def test_invalid_codes_and_turns():
-    b, t, _ = ops.reset(6, DEV)
-    r = ops.step(b, T([1, 1, 1, 0, 3, 2]), T([65, 200, 255, 19, 19, 64]))
-    assert r.ret.cpu().tolist() == [-1, -1, -1, -1, -1, 0]
-    assert (U(r.boards) == U(b)).all()
-    assert r.turn.cpu().tolist() == [1, 1, 1, 0, 3, 1]
+def test_invalid_codes_and_odd_turns():
+    """Codes > 64 are -1 with the state unchanged.  Side Empty (0) on the
+    opening: d3 flanks e4 (a Black run ending on the empty f5), so e4 is
+    "flipped" to Empty and the turn goes to Black (board.py:155-209); a side
+    no square holds (3) takes only a pass, which also hands over to Black."""
+    b, t, _ = ops.reset(8, DEV)
+    r = ops.step(b, T([1, 1, 1, 0, 3, 2, 3, 0]), T([65, 200, 255, 19, 19, 64, 64, 0]))
+    assert r.ret.cpu().tolist() == [-1, -1, -1, 1, -1, 0, 0, -1]
+    assert r.turn.cpu().tolist() == [1, 1, 1, 1, 3, 1, 1, 0]
+    bo = U(r.boards)
+    assert (bo[[0, 1, 2, 4, 5, 6, 7]] == U(b)[[0, 1, 2, 4, 5, 6, 7]]).all()
+    e4 = np.uint64(1 << (4 + 8 * 3))
+    assert bo[3, 0] == U(b)[3, 0] & ~e4 and bo[3, 1] == U(b)[3, 1]
+    assert U(r.flips)[3] == e4
 
 
 def test_inplace_step_aliasing():
@@ -339,10 +347,44 @@ def test_config3_full_size_properties():
     np.testing.assert_array_equal(hist[:129], np.bincount(a.diff.cpu().numpy().astype(np.int64) + 64, minlength=129))
     # game length statistics of random play (mean 60.41, max 65)
     assert 60.0 < hist[132] / n < 61.0
-    # a 1% sample checked against the oracle
-    idx = np.arange(0, n, 97)
-    o = oracle.rollout(len(idx), 0x5EED, 0)  # contiguous ids 0..len-1
-    assert (U(a.final_boards)[:len(idx)] == o["final_boards"]).all()
+    # a 1% sample spread over the whole launch (stride 97 from both ends, so
+    # the batches dequeued last and the final partial wave are in it) against
+    # the oracle
+    _oracle_sample(a, n, 0x5EED, 0, 10, stride=97)
+
+
+def _oracle_sample(res, n, seed, policy, n_random, stride, weights=None):
+    idx = np.unique(np.concatenate([np.arange(0, n, stride), n - 1 - np.arange(0, n, stride)]))
+    o = oracle.rollout_ids(idx, seed, policy, n_random, weights=weights)
+    np.testing.assert_array_equal(U(res.final_boards)[idx], o["final_boards"])
+    np.testing.assert_array_equal(res.diff.cpu().numpy()[idx], o["diff"])
+    np.testing.assert_array_equal(res.plies.cpu().numpy()[idx], o["plies"])
+
+
+@pytest.mark.parametrize("policy", ["greedy", "eval"])
+def test_config5_full_size_properties(policy):
+    """batch 1,048,576 with the 1-ply policies (config 5 and the eval player):
+    determinism, split invariance, terminal finals, histogram consistency, and
+    a strided oracle sample over the whole launch."""
+    from subproc_amd.params import DEFAULT_WEIGHTS
+    w = DEFAULT_WEIGHTS if policy == "eval" else None
+    pid = {"greedy": 1, "eval": 2}[policy]
+    n = 1 << 20
+    a = ops.rollout(n, 0x5EED, 0, policy, 10, device=DEV, weights=w)
+    b = ops.rollout(n, 0x5EED, 0, policy, 10, device=DEV, weights=w)
+    assert torch.equal(a.final_boards, b.final_boards) and torch.equal(a.hist, b.hist)
+    k = 333_333
+    h1 = ops.rollout(k, 0x5EED, 0, policy, 10, device=DEV, weights=w)
+    h2 = ops.rollout(n - k, 0x5EED, k, policy, 10, device=DEV, weights=w)
+    assert torch.equal(torch.cat([h1.final_boards, h2.final_boards]), a.final_boards)
+    assert torch.equal(h1.hist + h2.hist, a.hist)
+    res = ops.result(a.final_boards)
+    assert bool(res.terminal.bool().all()) and torch.equal(res.diff, a.diff)
+    hist = a.hist.cpu().numpy()
+    assert hist[:129].sum() == n and hist[129:132].sum() == n
+    assert hist[132] == int(a.plies.long().sum())
+    np.testing.assert_array_equal(hist[:129], np.bincount(a.diff.cpu().numpy().astype(np.int64) + 64, minlength=129))
+    _oracle_sample(a, n, 0x5EED, pid, 10, stride=257, weights=w)
 
 
 def test_config4_global_histogram_equals_shards():
@@ -392,8 +434,8 @@ def test_rollout_game_ids_wrap_2_64():
 
 
 def test_concurrent_rollouts_on_two_streams():
-    """Launches in flight together use separate work counters (g_work slots):
-    results equal the same launches run one after the other."""
+    """Launches in flight together use separate work words (one per stream,
+    ops.work_word): results equal the same launches run one after the other."""
     n = 1 << 18
     seq = [ops.rollout(n, 77, k * n, "random", device=DEV) for k in range(2)]
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -417,40 +459,75 @@ def test_mixed_device_and_cpu_arguments_are_rejected():
     assert int(r.hist[:129].sum()) == 8
 
 
-def test_counter_slots_survive_reuse():
-    """oth_rollout keeps no reset on the stream: each of the 64 work-counter slots
-    advances by a host-tracked 64 * (batches + waves) per launch.  130 launches
-    (every slot reused twice, sizes varying) must all equal their reference."""
+def test_work_word_returns_to_zero_across_sizes():
+    """A launch leaves its work word at 0 (the last dequeue resets it), so one
+    word serves any sequence of launches on a stream: 130 launches of varying
+    sizes and policies all equal their reference."""
     ref = {n: ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False).hist
            for n in (1, 64, 1000, 5000)}
+    w = torch.zeros(1, dtype=torch.int64, device=DEV)
     for k in range(130):
         n = (1, 64, 1000, 5000)[k % 4]
-        r = ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False)
+        r = ops.rollout(n, 3, 1000, device=DEV, want_boards=False, want_plies=False, work=w)
         assert torch.equal(r.hist, ref[n]), (k, n)
+        if k % 13 == 0:
+            ops.rollout(777, 4, 0, "greedy", 10, device=DEV, work=w)
+    assert int(w.item()) == 0
+
+
+def test_many_rollouts_in_flight_on_several_streams():
+    """96 launches (more than the 64 the r1 slot table allowed) in flight on 4
+    streams, each stream with its own work word; stream 1 starts behind a
+    sleep so later launches on the other streams overtake its earlier ones.
+    Every launch equals the same launch run alone."""
+    n = 3000
+    ids = [(k * 7919) % 50000 for k in range(96)]
+    ref = [ops.rollout(n, 21, g, device=DEV, want_diff=False, want_plies=False) for g in ids[:8]]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(streams[1]):
+        torch.cuda._sleep(50_000_000)  # ~20 ms: the other streams run ahead
+    outs = []
+    for k, g in enumerate(ids):
+        with torch.cuda.stream(streams[k % 4]):
+            outs.append(ops.rollout(n, 21, g, device=DEV, want_diff=False, want_plies=False))
+    torch.cuda.synchronize()
+    for k in range(8):
+        assert torch.equal(outs[k].final_boards, ref[k].final_boards) and torch.equal(outs[k].hist, ref[k].hist), k
+    for k in range(8, 96):
+        assert int(outs[k].hist[:129].sum()) == n, k  # no game dropped
+        if k % 8 == 0:
+            alone = ops.rollout(n, 21, ids[k], device=DEV, want_diff=False, want_plies=False)
+            assert torch.equal(outs[k].final_boards, alone.final_boards), k
+    for st in streams:
+        with torch.cuda.stream(st):
+            assert int(ops.work_word(DEV).item()) == 0
 
 
 def test_rollout_captured_in_a_graph_replays_correctly():
-    """A captured oth_rollout records its own counter reset (graph slots), so
-    every replay plays all games; eager launches on the normal slots before and
-    after the replays are unaffected."""
+    """A captured oth_rollout needs no reset node: each replay finds its work
+    word at 0 and leaves it at 0, so every replay plays all games; eager
+    launches before and after the replays are unaffected."""
     n = 3000
     ref = ops.rollout(n, 9, 50, device=DEV)
     fb = torch.empty((n, 2), dtype=torch.int64, device=DEV)
     hist = torch.zeros(133, dtype=torch.int64, device=DEV)
+    w = torch.zeros(1, dtype=torch.int64, device=DEV)
     from subproc_amd import _lib
     lib = _lib.load()
     g = torch.cuda.CUDAGraph()
     torch.cuda.synchronize()
     with torch.cuda.graph(g):
         st = torch.cuda.current_stream().cuda_stream
-        _lib.check(lib.oth_rollout(None, None, 9, 50, 0, 10, fb.data_ptr(), None, None, None, hist.data_ptr(), n, st),
-                   "oth_rollout")
+        _lib.check(lib.oth_rollout(None, None, 9, 50, 0, 10, fb.data_ptr(), None, None, None, hist.data_ptr(),
+                                   w.data_ptr(), n, st), "oth_rollout")
     for k in range(3):
         hist.zero_()
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(fb, ref.final_boards), k
         assert torch.equal(hist, ref.hist), k
+        assert int(w.item()) == 0
         mid = ops.rollout(n, 9, 50, device=DEV)
         assert torch.equal(mid.hist, ref.hist), k
 

@@ -14,13 +14,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&fb, n * 16)); CK(hipMalloc(&df, n)); CK(hipMalloc(&pl, n)); CK(hipMalloc(&hist, 133 * 8));
     const long long maxw = 1 << 20;
     CK(hipMalloc(&diag, maxw * 32));
+    uint64_t* work; CK(hipMalloc(&work, 8)); CK(hipMemset(work, 0, 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag)));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int r = 0; r < reps; r++) {
         CK(hipMemset(hist, 0, 133 * 8));
         CK(hipMemset(diag, 0, maxw * 32));
         CK(hipEventRecord(e0, 0));
-        int st = oth_rollout(nullptr, nullptr, 0x5EED, (uint64_t)r * n, 0, 10, fb, df, pl, nullptr, hist, n, nullptr);
+        int st = oth_rollout(nullptr, nullptr, 0x5EED, (uint64_t)r * n, 0, 10, fb, df, pl, nullptr, hist, work, n, nullptr);
         CK(hipEventRecord(e1, 0));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));

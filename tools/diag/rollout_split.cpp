@@ -169,8 +169,10 @@ int main(int argc, char** argv) {
         const unsigned long long gid0 = (unsigned long long)r * n;
         CK(hipMemset(hist_ref, 0, 133 * 8));
         CK(hipEventRecord(e0, 0));
-        int st = oth_rollout(nullptr, nullptr, 0x5EED, gid0, 0, 0, nullptr, nullptr, nullptr, nullptr, hist_ref, n,
-                             nullptr);
+        static uint64_t* ref_work = nullptr;
+        if (!ref_work) { CK(hipMalloc(&ref_work, 8)); CK(hipMemset(ref_work, 0, 8)); }
+        int st = oth_rollout(nullptr, nullptr, 0x5EED, gid0, 0, 0, nullptr, nullptr, nullptr, nullptr, hist_ref, ref_work,
+                             n, nullptr);
         CK(hipEventRecord(e1, 0));
         CK(hipDeviceSynchronize());
         float ms_ref;

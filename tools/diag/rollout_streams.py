@@ -17,6 +17,7 @@ dev = torch.device("cuda", 0)
 streams = [torch.cuda.Stream(dev) for _ in range(4)]
 bufs = [(torch.empty((n, 2), dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int8, device=dev),
          torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(4)]
+works = torch.zeros(4, dtype=torch.int64, device=dev)  # one rollout work word per stream
 
 
 def run(S, gid0):
@@ -27,7 +28,8 @@ def run(S, gid0):
         st = streams[s % S]
         fb, df, pl = bufs[s % S]
         _lib.check(lib.oth_rollout(None, None, 0x5EED, gid0 + s * n, 0, 10, fb.data_ptr(), df.data_ptr(),
-                                   pl.data_ptr(), None, hists[s].data_ptr(), n, st.cuda_stream), "oth_rollout")
+                                   pl.data_ptr(), None, hists[s].data_ptr(), works[s % S:s % S + 1].data_ptr(), n,
+                                   st.cuda_stream), "oth_rollout")
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return dt, hists.cpu()

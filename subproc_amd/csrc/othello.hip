@@ -694,85 +694,185 @@ __global__ __launch_bounds__(kBlock) void sample_midgame_kernel(u64 S, u64 index
 // position (game_runner.py:169-184 records the board after Board() and after
 // every put_s), with is_game_over per position (game_recorder.py:107-114).
 // ---------------------------------------------------------------------------
-// One lane per game.  A lane's rows are its own (stride OTH_POS_STRIDE), so a
-// store instruction touches 64 different lines; positions are therefore
-// buffered kReplayBurst at a time and written back to back, so each 128-B line
-// of the board rows is completed while it is still in L2 (one row store per
-// position let half-written lines be evicted: 3.4 GB of HBM traffic per
-// 262,144-game launch against 0.64 GB written).
-constexpr int kReplayBurst = 8;
-__global__ __launch_bounds__(kBlock) void replay_kernel(const u64* __restrict__ start,
+// One lane per game; HBM traffic is kept to the bytes the ABI defines:
+//  * board rows: a lane's rows are its own (stride OTH_POS_STRIDE), so one
+//    store instruction touches 64 different lines.  Positions are buffered
+//    8 at a time, and the bursts are aligned so that each one fills exactly
+//    one 128-B line (row i*129 + p starts a line when (i + p) % 8 == 0, since
+//    129 = 1 mod 8): every line is written whole by 8 back-to-back stores
+//    instead of lingering half-written in L2 (one store per position let
+//    partial lines be evicted: 3.4 GB of traffic per 262,144-game launch for
+//    0.64 GB of output);
+//  * move codes: the lane's 128-B record is read once, by 8 dwordx4 loads, into
+//    a register shift register (a byte load per position re-fetched lines the
+//    L2 had evicted in between);
+//  * turn / end bytes: staged in LDS as one packed byte per position (turn in
+//    bits 0-6, is_game_over in bit 7) at the block's own output layout, then
+//    written out as the block's two contiguous ranges by coalesced 16-B stores
+//    (per-lane byte stores at stride 129 touched a line per lane per position).
+//    Rows past plies are written as 0.  A turn >= 127 can only be the game's
+//    start turn (put_s sets the turn to Black or White), so it is staged as the
+//    escape 127 and restored from start_turn on the way out.
+constexpr int kReplayBurst = 8;                         // positions per burst: one 128-B line of rows
+constexpr int kReplayStage = kBlock * OTH_POS_STRIDE;  // packed turn/end bytes of one block
+constexpr u32 kTurnEscape = 0x7f;
+static_assert(kReplayStage % 16 == 0, "block stage = whole 16-B chunks");
+
+__device__ __forceinline__ void load_move_record(const uint8_t* row, bool vec, u64 (&R)[OTH_MOVES_STRIDE / 8]) {
+    if (vec) {
+        const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(row);
+#pragma unroll
+        for (int j = 0; j < OTH_MOVES_STRIDE / 16; j++) {
+            const ulonglong2 v = r2[j];
+            R[2 * j] = v.x;
+            R[2 * j + 1] = v.y;
+        }
+    } else {  // a caller's record that is not 16-B aligned
+#pragma unroll
+        for (int j = 0; j < OTH_MOVES_STRIDE / 8; j++) {
+            u64 w = 0;
+#pragma unroll 1
+            for (int k = 0; k < 8; k++) w |= (u64)row[8 * j + k] << (8 * k);
+            R[j] = w;
+        }
+    }
+}
+
+// byte q of a staged block (game q / 129 of the block) -> (turn, end)
+__device__ __forceinline__ void unstage_byte(u32 c, const uint8_t* start_turn, int64_t game, uint8_t& t, uint8_t& e) {
+    const u32 tt = c & kTurnEscape;
+    t = (uint8_t)(tt == kTurnEscape ? start_turn[game] : tt);
+    e = (uint8_t)(c >> 7);
+}
+
+__global__ __launch_bounds__(kBlock, 4) void replay_kernel(const u64* __restrict__ start,
                                                         const uint8_t* __restrict__ start_turn,
                                                         const uint8_t* __restrict__ moves,
                                                         const uint8_t* __restrict__ plies, u64* __restrict__ pos,
                                                         uint8_t* __restrict__ pos_turn, uint8_t* __restrict__ pos_end,
-                                                        int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
-    u32 t = OTH_BLACK;
-    if (start) {
-        const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(start)[i];
-        bl = s0.x;
-        wh = s0.y;
-        t = start_turn ? start_turn[i] : OTH_BLACK;
+                                                        int64_t n, int vec_moves, int vec_out) {
+    extern __shared__ uint4 replay_stage4[];  // kReplayStage bytes when turn or end is wanted
+    uint8_t* stage = reinterpret_cast<uint8_t*>(replay_stage4);
+    const bool staged = pos_turn || pos_end;
+    const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
+    const int nb = (int)min<int64_t>(kBlock, n - blk0);
+    const int lane = threadIdx.x;
+    if (staged) {
+        for (int c = lane; c < kReplayStage / 16; c += kBlock) replay_stage4[c] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
     }
-    const u32 np = min<u32>(plies[i], OTH_MOVES_STRIDE);
-    const uint8_t* mv = moves + i * OTH_MOVES_STRIDE;
-    ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
-    uint8_t* out_t = pos_turn ? pos_turn + i * OTH_POS_STRIDE : nullptr;
-    uint8_t* out_e = pos_end ? pos_end + i * OTH_POS_STRIDE : nullptr;
-    for (u32 p0 = 0; p0 <= np; p0 += kReplayBurst) {
-        ulonglong2 b[kReplayBurst];
-        uint8_t tt[kReplayBurst], ee[kReplayBurst];
-        const u32 m = min<u32>(kReplayBurst, np + 1 - p0);  // positions in this burst
+    if (lane < nb) {
+        const int64_t i = blk0 + lane;
+        u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
+        u32 t = OTH_BLACK;
+        if (start) {
+            const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(start)[i];
+            bl = s0.x;
+            wh = s0.y;
+            t = start_turn ? start_turn[i] : OTH_BLACK;
+        }
+        const int np = min<int>(plies[i], OTH_MOVES_STRIDE);
+        u64 R[OTH_MOVES_STRIDE / 8];
+        load_move_record(moves + i * OTH_MOVES_STRIDE, vec_moves != 0, R);
+        ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
+        uint8_t* st = stage + lane * OTH_POS_STRIDE;
+        const int s = (int)(i & 7);  // the first burst starts at p = -s: whole lines from there on
+        u64 prev = 0, cur = R[0];   // move-record words w[b-1], w[b] of burst b
+        for (int p0 = -s; p0 <= np; p0 += kReplayBurst) {
+            // move codes p0 .. p0+7 (bytes before position 0 are never used)
+            const u64 win = s ? (cur << (8 * s)) | (prev >> (64 - 8 * s)) : cur;
+            ulonglong2 b[kReplayBurst];
 #pragma unroll
-        for (u32 k = 0; k < kReplayBurst; k++) {
-            if (k < m) {
-                b[k] = make_ulonglong2(bl, wh);
-                tt[k] = (uint8_t)t;
-                ee[k] = (moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0) ? 1 : 0;
-                // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
-                const u32 p = p0 + k;
-                if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
-                    const StepOut o = put_s_any(bl, wh, t, mv[p]);  // side Empty / none (rare)
-                    bl = o.bl;
-                    wh = o.wh;
-                    t = o.t;
-                } else if (p < np) {
-                    const u32 c = mv[p];
-                    if (c == OTH_PASS) {
-                        t ^= 3u;
-                    } else if (c < 64) {
-                        const bool black = t == OTH_BLACK;
-                        u64 P = black ? bl : wh, O = black ? wh : bl;
-                        const u64 mm = 1ull << c;
-                        if (!((P | O) & mm)) {
-                            const u64 f = flips_carry(c, P, O);
-                            if (f) {
-                                P |= f | mm;
-                                O = andn(O, f);
-                                bl = black ? P : O;
-                                wh = black ? O : P;
-                                t ^= 3u;
+            for (int k = 0; k < kReplayBurst; k++) {
+                const int p = p0 + k;
+                if (p >= 0 && p <= np) {
+                    b[k] = make_ulonglong2(bl, wh);
+                    if (staged) {
+                        const u32 e = pos_end && moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0;
+                        st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
+                    }
+                    // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
+                    const u32 c = (u32)(win >> (8 * k)) & 0xffu;
+                    if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
+                        const StepOut o = put_s_any(bl, wh, t, c);  // side Empty / none (rare)
+                        bl = o.bl;
+                        wh = o.wh;
+                        t = o.t;
+                    } else if (p < np) {
+                        if (c == OTH_PASS) {
+                            t ^= 3u;
+                        } else if (c < 64) {
+                            const bool black = t == OTH_BLACK;
+                            u64 P = black ? bl : wh, O = black ? wh : bl;
+                            const u64 mm = 1ull << c;
+                            if (!((P | O) & mm)) {
+                                const u64 f = flips_carry(c, P, O);
+                                if (f) {
+                                    P |= f | mm;
+                                    O = andn(O, f);
+                                    bl = black ? P : O;
+                                    wh = black ? O : P;
+                                    t ^= 3u;
+                                }
                             }
                         }
                     }
                 }
             }
+#pragma unroll
+            for (int k = 0; k < kReplayBurst; k++) {
+                const int p = p0 + k;
+                if (p >= 0 && p <= np) out[p] = b[k];
+            }
+            prev = cur;
+#pragma unroll
+            for (int j = 0; j < OTH_MOVES_STRIDE / 8 - 1; j++) R[j] = R[j + 1];
+            R[OTH_MOVES_STRIDE / 8 - 1] = 0;
+            cur = R[0];
         }
+    }
+    if (!staged) return;
+    __syncthreads();
+    // the block's rows of pos_turn / pos_end are one contiguous range each
+    const int bytes = nb * OTH_POS_STRIDE;
+    const int64_t base = blk0 * OTH_POS_STRIDE;
+    if (vec_out) {
+        for (int c = lane; c * 16 < bytes; c += kBlock) {
+            const uint4 v = replay_stage4[c];
+            u32 w[4] = {v.x, v.y, v.z, v.w};
+            u32 tw[4], ew[4];
+            bool esc = false;
 #pragma unroll
-        for (u32 k = 0; k < kReplayBurst; k++)
-            if (k < m) out[p0 + k] = b[k];
-        if (out_t) {
+            for (int q = 0; q < 4; q++) {
+                tw[q] = w[q] & 0x7f7f7f7fu;
+                ew[q] = (w[q] >> 7) & 0x01010101u;
+                esc |= ((tw[q] + 0x01010101u) & 0x80808080u) != 0;  // a byte == 0x7f
+            }
+            if (esc) {  // rare: a start turn >= 127 still to move
 #pragma unroll
-            for (u32 k = 0; k < kReplayBurst; k++)
-                if (k < m) out_t[p0 + k] = tt[k];
+                for (int q = 0; q < 16; q++) {
+                    const int o = c * 16 + q;
+                    uint8_t tb, eb;
+                    unstage_byte(w[q >> 2] >> (8 * (q & 3)) & 0xffu, start_turn, blk0 + o / OTH_POS_STRIDE, tb, eb);
+                    tw[q >> 2] = (tw[q >> 2] & ~(0xffu << (8 * (q & 3)))) | ((u32)tb << (8 * (q & 3)));
+                }
+            }
+            if ((c + 1) * 16 <= bytes) {
+                if (pos_turn) *reinterpret_cast<uint4*>(pos_turn + base + c * 16) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+                if (pos_end) *reinterpret_cast<uint4*>(pos_end + base + c * 16) = make_uint4(ew[0], ew[1], ew[2], ew[3]);
+            } else {  // the launch's last partial chunk
+                for (int q = 0; c * 16 + q < bytes; q++) {
+                    if (pos_turn) pos_turn[base + c * 16 + q] = (uint8_t)(tw[q >> 2] >> (8 * (q & 3)));
+                    if (pos_end) pos_end[base + c * 16 + q] = (uint8_t)(ew[q >> 2] >> (8 * (q & 3)));
+                }
+            }
         }
-        if (out_e) {
-#pragma unroll
-            for (u32 k = 0; k < kReplayBurst; k++)
-                if (k < m) out_e[p0 + k] = ee[k];
+    } else {  // a caller's output that is not 16-B aligned: coalesced byte stores
+        for (int o = lane; o < bytes; o += kBlock) {
+            uint8_t tb, eb;
+            unstage_byte(stage[o], start_turn, blk0 + o / OTH_POS_STRIDE, tb, eb);
+            if (pos_turn) pos_turn[base + o] = tb;
+            if (pos_end) pos_end[base + o] = eb;
         }
     }
 }
@@ -1332,8 +1432,11 @@ int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* 
                uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!moves || !plies || !pos_boards))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    replay_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(start, start_turn, moves, plies, pos_boards,
-                                                                     pos_turn, pos_end, n);
+    const bool staged = pos_turn || pos_end;
+    const int vec_moves = ((uintptr_t)moves & 15) == 0;
+    const int vec_out = (((uintptr_t)pos_turn | (uintptr_t)pos_end) & 15) == 0;
+    replay_kernel<<<blocks_for(n), kBlock, staged ? kReplayStage : 0, (hipStream_t)stream>>>(
+        start, start_turn, moves, plies, pos_boards, pos_turn, pos_end, n, vec_moves, vec_out);
     return launched();
 }
 

@@ -265,7 +265,8 @@ def replay(moves, plies, start=None, start_turn=None):
     """Every recorded position of n games (GameRunner records the board after
     Board() and after each put_s, game_runner.py:169-184).  Returns Replay with
     boards (n, 129, 2) int64, turn (n, 129) uint8, end (n, 129) uint8 =
-    is_game_over(); game i's positions are rows 0..plies[i]."""
+    is_game_over(); game i's positions are rows 0..plies[i] (later rows: boards 0,
+    turn 0, end 0)."""
     n = moves.shape[0]
     pm = _dev(moves, "moves", torch.uint8, (n, MOVES_STRIDE))
     pp = _dev(plies, "plies", torch.uint8, (n,), moves.device)
@@ -273,8 +274,8 @@ def replay(moves, plies, start=None, start_turn=None):
     pst = _opt(start_turn, "start_turn", torch.uint8, (n,), moves.device)
     dev = moves.device
     b = torch.zeros((n, POS_STRIDE, 2), dtype=torch.int64, device=dev)
-    t = torch.zeros((n, POS_STRIDE), dtype=torch.uint8, device=dev)
-    e = torch.zeros((n, POS_STRIDE), dtype=torch.uint8, device=dev)
+    t = torch.empty((n, POS_STRIDE), dtype=torch.uint8, device=dev)  # rows past plies: written as 0
+    e = torch.empty((n, POS_STRIDE), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
         check(_lib.load().oth_replay(ps, pst, pm, pp, b.data_ptr(), t.data_ptr(), e.data_ptr(), n, _stream()),
               "oth_replay")

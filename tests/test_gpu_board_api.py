@@ -101,6 +101,7 @@ def test_replay_from_side_empty_starts_vs_oracle():
     n = 2048
     pos = ops.sample_midgame(n, 17, device=DEV)
     st = np.where(rng.random(n) < 0.5, 0, rng.integers(0, 5, n)).astype(np.uint8)
+    st[::7] = rng.choice([126, 127, 128, 200, 255], len(st[::7]))  # turns the kernel stages as an escape
     moves = rng.integers(0, 66, (n, 128)).astype(np.uint8)
     plies = rng.integers(0, 129, n).astype(np.uint8)
     r = ops.replay(T(moves), T(plies), start=pos.boards, start_turn=T(st))
@@ -116,3 +117,35 @@ def API_BLACK():
 
 def API_WHITE():
     return load_npz("board_api.npz")["white"]
+
+
+@pytest.mark.parametrize("n", [1, 255, 257, 1000])
+def test_replay_unaligned_buffers_and_ragged_blocks_vs_oracle(n):
+    """oth_replay with move records and turn/end outputs that are not 16-B
+    aligned (the kernel's byte paths), block-ragged n, start turns >= 127, and
+    outputs pre-filled with garbage: rows past plies read back as 0."""
+    from subproc_amd import _lib
+
+    rng = np.random.default_rng(n)
+    pos = ops.sample_midgame(n, 23, device=DEV)
+    st = rng.choice([0, 1, 2, 3, 127, 255], n).astype(np.uint8)
+    moves = rng.integers(0, 66, (n, 128)).astype(np.uint8)
+    moves[rng.random((n, 128)) < 0.5] = 64  # plenty of passes: turns toggle early
+    plies = rng.integers(0, 129, n).astype(np.uint8)
+    o = oracle.replay(moves, plies, start=U(pos.boards), start_turn=st)
+    for off in (0, 1, 3):
+        mv = torch.zeros(n * 128 + off, dtype=torch.uint8, device=DEV)
+        mv[off:] = T(moves.reshape(-1))
+        pb = torch.zeros((n, 129, 2), dtype=torch.int64, device=DEV)
+        pt = torch.full((n * 129 + off,), 0xAB, dtype=torch.uint8, device=DEV)
+        pe = torch.full((n * 129 + off,), 0xCD, dtype=torch.uint8, device=DEV)
+        stt, pl = T(st), T(plies)
+        rc = _lib.load().oth_replay(pos.boards.data_ptr(), stt.data_ptr(), mv.data_ptr() + off, pl.data_ptr(),
+                                    pb.data_ptr(), pt.data_ptr() + off, pe.data_ptr() + off, n,
+                                    torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(U(pb), o["boards"], err_msg=f"off {off}")
+        np.testing.assert_array_equal(pt[off:].cpu().numpy().reshape(n, 129), o["turn"], err_msg=f"off {off}")
+        np.testing.assert_array_equal(pe[off:].cpu().numpy().reshape(n, 129), o["end"], err_msg=f"off {off}")
+        assert (pt[:off].cpu().numpy() == 0xAB).all() and (pe[:off].cpu().numpy() == 0xCD).all()

@@ -45,8 +45,9 @@ class Engine:
         self.weights = params.as_weights(params.DEFAULT_WEIGHTS if weights is None else weights)
         self.board = gboard.Board()
 
-    def _choose_eval(self, puts):
-        """All children in one oth_step launch, their evals in one oth_eval launch."""
+    def _children(self, puts, want_legal):
+        """Every child of the side to move in ONE oth_step launch (board
+        repeated per legal square): the StepResult on the device."""
         b = self.board
         bl, wh = b.bitboards()
         n = len(puts)
@@ -54,9 +55,21 @@ class Engine:
         boards = ops.from_numpy_u64(np.array([[bl, wh]] * n, np.uint64), dev)
         side = torch.full((n,), b.turn, dtype=torch.uint8, device=dev)
         sq = torch.tensor([x + 8 * y for (x, y) in puts], dtype=torch.uint8, device=dev)
-        children = ops.step(boards, side, sq, want_flips=False, want_legal=False).boards
-        ev = ops.evaluate(children, side, self.weights).cpu().tolist()
-        k = max(range(n), key=lambda i: (ev[i], -i))  # puts is LSB-first: ties -> lowest square
+        return ops.step(boards, side, sq, want_flips=False, want_legal=want_legal), side
+
+    def _choose_eval(self, puts):
+        """The children's evals in one more oth_eval launch."""
+        r, side = self._children(puts, want_legal=False)
+        ev = ops.evaluate(r.boards, side, self.weights).cpu().tolist()
+        k = max(range(len(puts)), key=lambda i: (ev[i], -i))  # puts is LSB-first: ties -> lowest square
+        return handstr_from_coord(*puts[k])
+
+    def _choose_greedy(self, puts):
+        """A legal move hands the turn over, so each child's legal_next is the
+        opponent's puttables: its popcount is n_puttable_for(hostile)."""
+        r, _ = self._children(puts, want_legal=True)
+        mob = [bin(v & (2**64 - 1)).count("1") for v in r.legal_next.cpu().tolist()]
+        k = min(range(len(puts)), key=lambda i: (mob[i], i))  # ties -> lowest square
         return handstr_from_coord(*puts[k])
 
     def choose(self):
@@ -69,17 +82,7 @@ class Engine:
             return handstr_from_coord(x, y)
         if self.policy == "eval":
             return self._choose_eval(puts)
-        best, bestv = None, None
-        opp = b.hostile(b.turn)
-        for (x, y) in puts:
-            c = gboard.Board()
-            c.board = b.board
-            c.turn = b.turn
-            c.put_s(handstr_from_coord(x, y))
-            v = c.n_puttable_for(opp)
-            if bestv is None or v < bestv:
-                best, bestv = (x, y), v
-        return handstr_from_coord(*best)
+        return self._choose_greedy(puts)
 
     def handle(self, line, out):
         cmd = line.strip()

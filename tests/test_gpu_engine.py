@@ -127,3 +127,21 @@ def test_engine_eval_process_with_paramgen_file(tmp_path):
             if p.proc.poll() is None:
                 p.proc.kill()
     assert final.is_game_over() and black.name == "GPU-eval"
+
+
+def test_engine_greedy_choice_equals_kernel_policy():
+    """--policy greedy (all children in one oth_step launch, mobility from
+    legal_next) picks exactly what the kernels' greedy policy picks: the first
+    move of a greedy rollout with n_random = 0 from the same position."""
+    from subproc_amd import engine, ops
+    eng = engine.Engine(policy="greedy")
+    n = 64
+    pos = ops.sample_midgame(n, 78, device="cuda")
+    r = ops.rollout(n, 5, 0, "greedy", 0, start=pos.boards, start_turn=pos.turn, record_moves=True, device="cuda")
+    first = r.moves[:, 0].cpu().tolist()
+    bits = ops.to_numpy_u64(pos.boards)
+    for i in range(n):
+        eng.board = gboard.Board()
+        eng.board._set_bits(int(bits[i, 0]), int(bits[i, 1]))
+        eng.board.turn = int(pos.turn[i])
+        assert codec.move_code(eng.choose().lower()) == first[i], i

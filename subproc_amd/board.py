@@ -76,56 +76,116 @@ def _side_code(piece):
 
 
 class _Device:
-    """Resident batch-of-one device buffers shared by all Board instances."""
+    """The HIP library for batch-of-one calls: fixed pinned / device staging
+    buffers, raw C-ABI launches on torch's current stream, one host sync per
+    call, and an analysis cache.
+
+    A GameRunner ply asks puttables(turn), put_s and is_game_over
+    (game_runner.py:137-158).  ``step`` therefore also analyses the position it
+    produces -- both sides' legal masks, disc counts, is_game_over -- in the
+    same sync (oth_step, 2 x oth_legal, oth_result), and the next questions
+    about that position are answered from the cache: one sync per ply.
+
+    Staging layout (int64 words; byte offsets for the uint8 arguments):
+      in : [0] black [1] white | byte 16 side code, 17 move, 18 = 1, 19 = 2
+      out: [0] black [1] white (step result) | [2] legal Black [3] legal White
+           [4] flips | byte 40 ret, 41 n_black, 42 n_white, 43 is_game_over
+    """
+
+    _CACHE_MAX = 1 << 16
 
     def __init__(self):
         import torch
 
-        from . import _lib, ops
+        from . import _lib
 
-        _lib.load()
+        self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.OthelloLibraryError("subproc_amd.board needs a ROCm GPU: there is no CPU path")
-        self.torch, self.ops = torch, ops
+        self.torch = torch
         self.dev = torch.device("cuda", torch.cuda.current_device())
-        self.boards = torch.empty((1, 2), dtype=torch.int64, device=self.dev)
-        self.turn = torch.empty(1, dtype=torch.uint8, device=self.dev)
-        self.move = torch.empty(1, dtype=torch.uint8, device=self.dev)
-        self.host = torch.empty(4, dtype=torch.int64).pin_memory()
+        self.hin = torch.zeros(4, dtype=torch.int64).pin_memory()
+        self.hout = torch.zeros(6, dtype=torch.int64).pin_memory()
+        self.din = torch.zeros(4, dtype=torch.int64, device=self.dev)
+        self.dout = torch.zeros(6, dtype=torch.int64, device=self.dev)
+        self.hin_w = self.hin.numpy()
+        self.hin_b = self.hin_w.view(np.uint8)
+        self.hout_w = self.hout.numpy().view(np.uint64)
+        self.hout_b = self.hout_w.view(np.uint8)
+        self.hin_b[18], self.hin_b[19] = Black, White
+        self.i, self.o = self.din.data_ptr(), self.dout.data_ptr()
+        self.cache = {}
+        self._check = _lib.check
 
-    def _load(self, black, white, turn=None, move=None):
-        h = self.host
-        h[0], h[1] = _i64(black), _i64(white)
-        h[2] = 0 if turn is None else turn
-        h[3] = 0 if move is None else move
-        self.boards.view(-1).copy_(h[:2], non_blocking=True)
-        self.turn.copy_(h[2:3], non_blocking=True)
-        self.move.copy_(h[3:4], non_blocking=True)
+    def _launch_in(self, black, white, code=0, move=0):
+        self.hin_w[0], self.hin_w[1] = _i64(black), _i64(white)
+        self.hin_b[16], self.hin_b[17] = code, move
+        self.din.copy_(self.hin, non_blocking=True)
+        return self.torch.cuda.current_stream().cuda_stream
+
+    def _analyse_on_device(self, boards_ptr, s):
+        L, o, i = self.lib, self.o, self.i
+        self._check(L.oth_legal(boards_ptr, i + 18, o + 16, 1, s), "oth_legal")
+        self._check(L.oth_legal(boards_ptr, i + 19, o + 24, 1, s), "oth_legal")
+        self._check(L.oth_result(boards_ptr, o + 41, o + 42, None, o + 43, 1, s), "oth_result")
+
+    def _fetch(self):
+        self.hout.copy_(self.dout, non_blocking=True)
+        self.torch.cuda.current_stream().synchronize()
+        w, b = self.hout_w, self.hout_b
+        return int(w[0]), int(w[1]), (int(w[2]), int(w[3]), int(b[41]), int(b[42]), bool(b[43])), int(w[4]), int(
+            b.view(np.int8)[40])
+
+    def _remember(self, key, analysis):
+        if len(self.cache) >= self._CACHE_MAX:
+            self.cache.clear()
+        self.cache[key] = analysis
+
+    def analyse(self, black, white):
+        """(legal Black, legal White, n_black, n_white, is_game_over) of a
+        board of Black, White and empty squares (board.py:37-58)."""
+        key = (black, white)
+        a = self.cache.get(key)
+        if a is None:
+            s = self._launch_in(black, white)
+            self._analyse_on_device(self.i, s)
+            a = self._fetch()[2]
+            self._remember(key, a)
+        return a
 
     def legal(self, black, white, code):
-        self._load(black, white, code)
-        return _u64(int(self.ops.legal(self.boards, self.turn).item()))
+        """puttables(piece) as a mask for any side code (oth_legal)."""
+        if code in (Black, White):
+            return self.analyse(black, white)[code - 1]
+        s = self._launch_in(black, white, code)
+        self._check(self.lib.oth_legal(self.i, self.i + 16, self.o + 16, 1, s), "oth_legal")
+        return self._fetch()[2][0]
 
     def result(self, black, white):
-        self._load(black, white)
-        r = self.ops.result(self.boards)
-        t = self.torch.stack([r.n_black.long(), r.n_white.long(), r.terminal.long()]).view(-1).tolist()
-        return t[0], t[1], bool(t[2])
+        a = self.analyse(black, white)
+        return a[2], a[3], a[4]
 
     def step(self, black, white, code, move):
-        self._load(black, white, code, move)
-        r = self.ops.step(self.boards, self.turn, self.move, want_legal=False)
-        v = self.torch.cat([r.boards.view(-1), r.flips, r.ret.long()]).tolist()
-        return _u64(v[0]), _u64(v[1]), _u64(v[2]), int(v[3])
+        """put_s (oth_step) -> (black, white, flips, ret); the position it
+        leaves is analysed in the same sync."""
+        s = self._launch_in(black, white, code, move)
+        L, i, o = self.lib, self.i, self.o
+        self._check(L.oth_step(i, i + 16, i + 17, o, None, o + 32, None, o + 40, None, 1, s), "oth_step")
+        self._analyse_on_device(o, s)
+        bl, wh, a, flips, ret = self._fetch()
+        self._remember((bl, wh), a)
+        return bl, wh, flips, ret
 
     def hands(self, own, hostile, rows):
         """rows: [(x, y, dx, dy), ...] with one own/hostile pair -> run lengths."""
+        from . import ops
+
         t = self.torch
         n = len(rows)
         a = t.tensor([[_i64(own), _i64(hostile), *r] for r in rows], dtype=t.int64).t().contiguous()
         a = a.pin_memory().to(self.dev, non_blocking=True)
-        out = self.ops.hands(a[0].contiguous(), a[1].contiguous(), a[2].contiguous(), a[3].contiguous(),
-                             a[4].contiguous(), a[5].contiguous())
+        out = ops.hands(a[0].contiguous(), a[1].contiguous(), a[2].contiguous(), a[3].contiguous(),
+                        a[4].contiguous(), a[5].contiguous())
         return out.cpu().tolist()[:n]
 
 
@@ -329,14 +389,13 @@ class Board:
 
     # ---------------------------------------------------------------- GPU-backed rules
     def _result(self):
-        k = ("result", self._black, self._white)
-        if k not in self._cache:
-            self._cache[k] = _device().result(self._black, self._white)
-        return self._cache[k]
+        return _device().result(self._black, self._white)
 
     def _legal(self, piece):
         code = _side_code(piece)
         if self._fast(piece):
+            if code in (Black, White):
+                return _device().legal(self._black, self._white, code)  # the device caches the analysis
             k = ("legal", self._black, self._white, code)
             if k not in self._cache:
                 self._cache[k] = _device().legal(self._black, self._white, code)

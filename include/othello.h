@@ -271,7 +271,10 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
  * upd_keys[0..j) are not in old_keys.  The output has n_old +
  * new_before[n_upd] entries and must not overlap the inputs.  Keys are
  * OTH_TD_KEY values.  This is the store write of every updated key
- * (progress_position_moves_learn.py:58-62) for a whole batch. */
+ * (progress_position_moves_learn.py:58-62) for a whole batch.
+ * new_before must be the exclusive cumsum of oth_td_lookup's is_new for the
+ * same two key lists: for any other array the GPU build's output is undefined
+ * (slots may stay unwritten), while the host build returns OTH_EINVAL. */
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
                  double* out_vals, void* stream);

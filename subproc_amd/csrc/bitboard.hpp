@@ -77,13 +77,34 @@ __device__ __forceinline__ PairProp pair_prop(u64 pro) {
     return q;
 }
 
+// one Kogge-Stone step gen |= pro & (gen shifted by K).  A shift by K >= 32
+// moves one half into the other and leaves zeros behind, and a zero half of the
+// shifted fill leaves that half of gen as it is: one 32-bit shift (none for
+// K = 32) and one v_bitop3_b32, against a 64-bit shift and two bitop3.
+template <int K, bool L>
+__device__ __forceinline__ u64 ks_step(u64 gen, u64 pro) {
+    if constexpr (K >= 32) {
+        u32 lo = (u32)gen, hi = (u32)(gen >> 32);
+        if (L) {
+            const u32 s = K == 32 ? lo : lo << (K - 32);
+            hi = (u32)__builtin_amdgcn_bitop3_b32((u32)(pro >> 32), s, hi, 0xCA);
+        } else {
+            const u32 s = K == 32 ? hi : hi >> (K - 32);
+            lo = (u32)__builtin_amdgcn_bitop3_b32((u32)pro, s, lo, 0xCA);
+        }
+        return ((u64)hi << 32) | lo;
+    } else {
+        return bfi(pro, sh<K, L>(gen), gen);
+    }
+}
+
 // occluded fill of `gen` along +S (L) or -S through the pair's propagators:
 // covers distances 0..7
 template <int S, bool L>
 __device__ __forceinline__ u64 ks(u64 gen, const PairProp& q) {
-    gen = bfi(q.pro, sh<S, L>(gen), gen);
-    gen = bfi(L ? q.p2L : q.p2R, sh<2 * S, L>(gen), gen);
-    gen = bfi(L ? q.p4L : q.p4R, sh<4 * S, L>(gen), gen);
+    gen = ks_step<S, L>(gen, q.pro);
+    gen = ks_step<2 * S, L>(gen, L ? q.p2L : q.p2R);
+    gen = ks_step<4 * S, L>(gen, L ? q.p4L : q.p4R);
     return gen;
 }
 
@@ -165,6 +186,10 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 // bit-reversed board.  Table rows: 0..2 = rays +8, +9, +7 (normal order),
 // 3..5 = rays -8, -9, -7 stored bit-reversed; 64 squares each (3 KiB).
 constexpr int kRayRows = 6;
+// the LDS table adds two rows per square: 6 = the square's bit, 7 = its bit
+// on the reversed board (1 << (63 - sq)); read with the rays, they replace two
+// variable 64-bit shifts of the VALU-bound loop by LDS reads
+constexpr int kTabRows = kRayRows + 2;
 __host__ __device__ inline u64 ray_from(int sq, int dx, int dy) {
     u64 r = 0;
     int x = sq & 7, y = sq >> 3;
@@ -177,13 +202,19 @@ __host__ __device__ inline u64 ray_from(int sq, int dx, int dy) {
     return r;
 }
 __device__ __forceinline__ void ray_table_init(u64* tab) {
-    for (int e = threadIdx.x; e < kRayRows * 64; e += blockDim.x) {
+    for (int e = threadIdx.x; e < kTabRows * 64; e += blockDim.x) {
         const int row = e >> 6, sq = e & 63;
         const int dx[6] = {0, 1, -1, 0, -1, 1}, dy[6] = {1, 1, 1, -1, -1, -1};
+        if (row >= kRayRows) {
+            tab[e] = 1ull << (row == kRayRows ? sq : 63 - sq);
+            continue;
+        }
         const u64 r = ray_from(sq, dx[row], dy[row]);
         tab[e] = row < 3 ? r : rev64(r);
     }
 }
+// the move's bit from the table (row kRayRows)
+__device__ __forceinline__ u64 square_bit(u32 sq, const u64* tab) { return tab[kRayRows * 64 + sq]; }
 __device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bitop3<0x80>(a, b, c); }
 __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
     const u64 x = andn(R, A);
@@ -210,7 +241,7 @@ __device__ __forceinline__ RunSets run_sets(const Position& s) {
 // The other six by the ray tables (run_prefix).
 __device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, const u64* tab) {
     u64 f = east_run(mv, r.A1);
-    u64 fr = east_run(1ull << (sq ^ 63u), r.rA0);  // west, in reversed space (rev64(mv))
+    u64 fr = east_run(tab[(kRayRows + 1) * 64 + sq], r.rA0);  // west, in reversed space (rev64(mv))
     f = or3(f, run_prefix(tab[0 * 64 + sq], r.A3), run_prefix(tab[1 * 64 + sq], r.A5));
     f |= run_prefix(tab[2 * 64 + sq], r.A7);
     fr = or3(fr, run_prefix(tab[3 * 64 + sq], r.rA2), run_prefix(tab[4 * 64 + sq], r.rA4));
@@ -302,9 +333,10 @@ __device__ __forceinline__ void kth_table_init(uint8_t* tab) {
         for (; k < 8; k++) tab[b * 8 + k] = 0;
     }
 }
-__device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, const uint8_t* tab) {
+// c_lo = __popc((u32)x), which the caller has from counting x (popcount_lo)
+__device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
     const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 c = __popc(lo);
+    u32 c = c_lo;
     bool up = k >= c;
     u32 w = up ? hi : lo;
     k = up ? k - c : k;

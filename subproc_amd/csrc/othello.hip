@@ -67,6 +67,12 @@ struct GameRng {
         return __umulhi(state, n);
     }
 };
+// the random rule's move: the k-th legal square, k uniform in [0, popcount)
+// (the low word's count is shared by the total and the k-th-bit search)
+__device__ __forceinline__ u32 pick_legal(u64 legal, GameRng& rng, const uint8_t* kth_tab) {
+    const u32 c_lo = __popc((u32)legal);
+    return kth_bit_tab(legal, rng.pick(c_lo + __popc((u32)(legal >> 32))), c_lo, kth_tab);
+}
 
 // counts() region masks a..h (parameter_progress_position_moves_learn.py:9-16)
 __constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
@@ -104,7 +110,7 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // choice: (score << 6) | square.
 template <int POLICY>
 __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab) {
-    const u64 mv = 1ull << sq;
+    const u64 mv = square_bit(sq, rays);
     const u64 f = flips_rays(sq, mv, s, rays);
     const u64 P2 = or3(P, f, mv), O2 = andn(O, f);
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
 #endif
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
-    __shared__ u64 rays[kRayRows * 64];
+    __shared__ u64 rays[kTabRows * 64];
     __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
     if (POLICY != OTH_POLICY_RANDOM && threadIdx.x < kBlock / 64) coop[threadIdx.x].total = 0;
@@ -548,8 +554,8 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         continue;
                     }
                     passed = false;
-                    const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
-                    const u64 mv = 1ull << sq;
+                    const u32 sq = pick_legal(legal, rng, kth_tab);
+                    const u64 mv = square_bit(sq, rays);
                     const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                     const u64 np = andn(O, f);
@@ -601,7 +607,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         if ((int)ply >= a.n_random)
                             choose = true;  // decided below, by the whole wave
                         else
-                            sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
+                            sq = pick_legal(legal, rng, kth_tab);
                     }
                 }
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
@@ -610,7 +616,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     if (choose) sq = c;
                 }
                 if (moving) {
-                    const u64 mv = 1ull << sq;
+                    const u64 mv = square_bit(sq, rays);
                     const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
                     const u64 np = andn(O, f);

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kBlock, 4) void split_kernel(u64 seed_state, u64 ga
                                                           long long* hist, unsigned* errors) {
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
-    __shared__ u64 rays[kRayRows * 64];
+    __shared__ u64 rays[kTabRows * 64];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
@@ -114,8 +114,8 @@ __global__ __launch_bounds__(kBlock, 4) void split_kernel(u64 seed_state, u64 ga
                 ply++;
                 passed = false;
             }
-            const u32 sq = kth_bit_tab(legal, rng.pick((u32)__popcll(legal)), kth_tab);
-            const u64 mv = 1ull << sq;
+            const u32 sq = pick_legal(legal, rng, kth_tab);
+            const u64 mv = square_bit(sq, rays);
             const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
             const u64 np = andn(O, f);
             O = P | f | mv;

@@ -363,7 +363,9 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     kname = "rollout_kernel<%d, false>" % pid
     pfile, kernels = load_profile()
     prof = profile_entry(kernels, kname, largest=True) if n == 1 << 20 else None
-    out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    # "bound" prices the launch's algorithmic HBM bytes (the contract's roofline);
+    # the resource that binds this kernel is VALU issue ("binding", and "valu")
+    out["roofline"] = {"bound": "hbm", "binding": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK_GBS,
                        "traffic": prof.get("hbm_bytes") if prof else None,
                        "kernel": kname, "launch_ms": launch_ms, "launch_ms_median": median_ms,

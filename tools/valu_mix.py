@@ -4,14 +4,11 @@ bench.py prices the integer kernels against (profiles/valu_mix.json).
 
 CDNA4 SIMDs are 32 lanes wide: a wave64 VALU instruction can issue every 2
 cycles (MI355X_MICROARCH.md, cycle constants).  Measured on the box
-(tools/diag/valu_rate*.cpp, DESIGN.md §3 cost model), only plain VOP2 logic
-(v_and/or/xor/not/mov) streams at ~2.2 cycles, v_bitop3_b32 at ~3.35;
-64-bit shifts, v_bfi_b32, v_or3_b32, v_bcnt, v_cndmask, 32-bit shifts and
-SGPR-operand forms take ~4 (table MEASURED).  So a kernel's ceiling is 1024
-SIMDs x clock / (mean cycles over its mix).
-Unmeasured VOP2 forms (add/sub/min/max) are counted as fast, which raises the
-ceiling (the conservative side for a fraction-of-peak claim).
-
+(tools/diag/valu_rate5.cpp, DESIGN.md §3 cost model), only bitwise logic and
+moves stream at ~2.2 cycles and v_bitop3_b32 at ~2.5 (4.3 with its three
+sources in one VGPR bank); shifts, bit reversal, popcount, selects, compares,
+multiplies and even 32-bit add/sub/min take 4.1-4.4.  So a kernel's ceiling is
+1024 SIMDs x clock / (mean cycles over its mix).
 The hot loop is the innermost LLVM loop (its header and every block tagged
 "in Loop: Header=<it>") holding the most VALU instructions; counts are static
 (every block once), so rarely-taken blocks inside the loop are included.
@@ -27,17 +24,33 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAST = re.compile(r"^v_(and|or|xor|not|mov|add|sub|subrev|min|max)_(b32|u32|i32|b64)_e32$")
-FAST_CYC, SLOW_CYC = 2.2, 4.0
-# measured issue cost of the instructions these kernels are made of (cycles per
-# wave-instruction per SIMD, 8 waves/SIMD, tools/diag/valu_rate4.cpp on the box);
-# anything else not FAST is SLOW_CYC
-MEASURED = {"v_bitop3_b32": 3.35, "v_bfi_b32": 4.2, "v_or3_b32": 4.2, "v_lshlrev_b64": 4.1, "v_lshrrev_b64": 4.15,
-            "v_lshl_add_u64": 4.65, "v_bfrev_b32_e32": 4.05, "v_alignbit_b32": 4.2, "v_perm_b32": 4.3,
-            "v_lshlrev_b32_e32": 4.0}
+# Measured on the box (tools/diag/valu_rate5.cpp: 32 independent instructions
+# on fixed registers, 8 waves/SIMD): only bitwise logic and moves stream at
+# ~2.2 cycles per wave-instruction; v_bitop3_b32 at 2.5 -- 4.3 when its three
+# source registers are distinct and in one VGPR bank (bank = number mod 4);
+# everything else these kernels use, 32-bit add/sub/min and compares
+# included, at 4.1-4.4.
+FAST = re.compile(r"^v_(and|or|xor|not|mov)_(b32|b64)(_e32)?$")
+FAST_CYC, SLOW_CYC = 2.2, 4.2
+BITOP3_CYC, BITOP3_CONFLICT_CYC = 2.5, 4.3
+MEASURED = {"v_lshlrev_b64": 4.25, "v_lshrrev_b64": 4.22, "v_lshl_add_u64": 4.24, "v_bfrev_b32_e32": 4.13,
+            "v_lshlrev_b32_e32": 4.07, "v_bcnt_u32_b32": 4.09, "v_mul_hi_u32": 4.29, "v_mad_u64_u32": 4.43,
+            "v_cndmask_b32_e64": 4.2, "v_bfe_u32": 4.25, "v_min_u32_e32": 4.08, "v_sub_u32_e32": 4.08,
+            "v_bfi_b32": 4.2, "v_or3_b32": 4.2, "v_alignbit_b32": 4.2, "v_perm_b32": 4.3}
 
 
-def cycles(op):
+def bank_conflict(line):
+    """three distinct source VGPRs in one bank (v_bitop3_b32 vD, vA, vB, vC)"""
+    m = re.match(r"\s*v_bitop3_b32\s+v\d+,\s*v(\d+),\s*v(\d+),\s*v(\d+)", line or "")
+    if not m:
+        return False
+    regs = {int(g) for g in m.groups()}
+    return len(regs) == 3 and len({r % 4 for r in regs}) == 1
+
+
+def cycles(op, line=None):
+    if op == "v_bitop3_b32":
+        return BITOP3_CONFLICT_CYC if bank_conflict(line) else BITOP3_CYC
     if op in MEASURED:
         return MEASURED[op]
     return FAST_CYC if FAST.match(op) else SLOW_CYC
@@ -89,7 +102,7 @@ def hot_loop_mix(body):
             continue
         m = re.match(r"^\s+(v_[a-z0-9_]+)", ln)
         if m and label:
-            blocks[label].append(m.group(1))
+            blocks[label].append((m.group(1), ln))
     loops = collections.defaultdict(list)
     for b, h in header_of.items():
         loops[h].extend(blocks[b])
@@ -97,11 +110,16 @@ def hot_loop_mix(body):
     if not inner:
         return None
     h, ops = max(inner.items(), key=lambda kv: len(kv[1]))
-    fast = sum(1 for o in ops if FAST.match(o))
-    slow = len(ops) - fast
-    mean = sum(cycles(o) for o in ops) / max(1, len(ops))
-    return {"loop_header": h, "valu": len(ops), "fast_vop2": fast, "slow": slow, "mean_cycles": round(mean, 3),
-            "top": collections.Counter(ops).most_common(8)}
+    return mix_of(ops, h)
+
+
+def mix_of(ops, header):
+    names = [o for o, _ in ops]
+    fast = sum(1 for o in names if FAST.match(o))
+    mean = sum(cycles(o, ln) for o, ln in ops) / max(1, len(ops))
+    return {"loop_header": header, "valu": len(ops), "fast_vop2": fast, "slow": len(ops) - fast,
+            "bitop3_bank_conflicts": sum(1 for o, ln in ops if o == "v_bitop3_b32" and bank_conflict(ln)),
+            "mean_cycles": round(mean, 3), "top": collections.Counter(names).most_common(8)}
 
 
 def main():
@@ -116,11 +134,8 @@ def main():
             if pat in name:
                 r = hot_loop_mix(body)
                 if r is None:  # no loop (elementwise kernels): the whole body
-                    ops = [m.group(1) for m in (re.match(r"^\s+(v_[a-z0-9_]+)", ln) for ln in body) if m]
-                    fast = sum(1 for o in ops if FAST.match(o))
-                    r = {"loop_header": None, "valu": len(ops), "fast_vop2": fast, "slow": len(ops) - fast,
-                         "mean_cycles": round(sum(cycles(o) for o in ops) / max(1, len(ops)), 3),
-                         "top": collections.Counter(ops).most_common(8)}
+                    ops = [(m.group(1), ln) for m, ln in ((re.match(r"^\s+(v_[a-z0-9_]+)", ln), ln) for ln in body) if m]
+                    r = mix_of(ops, None)
                 r["peak_winstr_s"] = out["simds"] * out["clock_ghz"] * 1e9 / r["mean_cycles"]
                 out["kernels"][k] = r
     json.dump(out, sys.stdout, indent=1)

@@ -527,11 +527,15 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     analyse(P, O, pos);
                     const u64 legal = pos.legal;
                     if (legal == 0) {
-                        if (passed) {
+                        // a full board is terminal at once: the other side has no
+                        // empty square either, so the hand-over iteration (a
+                        // second analysis) is skipped; 65% of random games end so
+                        const bool full = (P | O) == ~0ull;
+                        if (passed || full) {
                             // terminal: both sides without a legal move (board.py:57-58);
-                            // the pass handed over just before is not an env-step
+                            // a pass handed over just before is not an env-step
                             const bool p_black = (side0 == OTH_BLACK) == ((ply & 1u) == 0u);
-                            ply--;
+                            if (passed) ply--;
                             if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
                             const u64 bl = p_black ? P : O, wh = p_black ? O : P;
                             const int d = __popcll(bl) - __popcll(wh);
@@ -576,8 +580,9 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     analyse(P, O, pos);
                     const u64 legal = pos.legal;
                     if (legal == 0) {
-                        if (passed) {
-                            // terminal: both sides without a legal move (board.py:57-58)
+                        if (passed || (P | O) == ~0ull) {
+                            // terminal: both sides without a legal move (board.py:57-58);
+                            // a full board needs no hand-over iteration to know it
                             const u64 bl = side == OTH_BLACK ? P : O, wh = side == OTH_BLACK ? O : P;
                             const int d = __popcll(bl) - __popcll(wh);
                             if (a.final_boards)

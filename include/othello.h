@@ -90,7 +90,10 @@ int oth_legal(const uint64_t* boards, const uint8_t* turn, uint64_t* legal, int6
  * Outputs: boards_out (n,2), turn_out, flips (discs that changed, origin excluded),
  * legal_next = puttables(turn_out) on boards_out, ret.  Any output may be NULL.
  * boards_out may alias boards_in and turn_out may alias turn_in (in-place step).
- * nturn (may be NULL) is incremented in place where ret >= 0 (board.py:203-204). */
+ * nturn (may be NULL) is incremented in place where ret >= 0 (board.py:203-204);
+ * it is a byte and wraps mod 256, where board.py's int does not (a game to its
+ * end makes at most 60 placements plus its passes; only a caller that keeps
+ * passing on purpose reaches 256).  The Board facade keeps nturn as an int. */
 int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* move,
              uint64_t* boards_out, uint8_t* turn_out, uint64_t* flips, uint64_t* legal_next,
              int8_t* ret, uint8_t* nturn, int64_t n, void* stream);

@@ -139,18 +139,28 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 
 // Wave-cooperative choice.  A lane's own child loop makes the wave pay for its
 // busiest lane every ply (measured on greedy games: 662 child evaluations per
-// 64-game batch where 303 would do, 46% lane efficiency).  Instead every
-// choosing lane publishes its position and its (lane, square) children to the
-// wave's LDS area, all 64 lanes (finished games included) evaluate the
-// children round-robin, and each child's key is folded into its parent's slot
-// with an LDS atomicMin.  A wave whose children exceed the list falls back to
-// lane_choose for that ply (only possible from unusual start positions).
-constexpr int kCoopCap = 64 * 20;  // children per wave per ply (mean mobility ~8.4)
+// 64-game batch where 303 would do, 46% lane efficiency).  Instead the wave's
+// T children are spread over R = ceil(T / 64) rounds of all 64 lanes
+// (finished games included):
+//   * every choosing lane publishes its position (P, O, run sets) to the
+//     wave's LDS area, and evaluates its own children in its first rounds,
+//     taking them straight from its legal mask, lowest square first;
+//   * a lane with more than R children lists the surplus (its highest
+//     squares) in the wave's overflow list;
+//   * a lane with fewer than R children has R - (its children) free rounds,
+//     and the free rounds of the wave, numbered by an LDS atomic, take the
+//     overflow list entry of the same number;
+// and each child's key is folded into its parent's slot with an LDS atomicMin
+// (so the order in which children are evaluated does not matter).  Only the
+// surplus is listed: listing every child cost a per-lane loop as long as the
+// busiest lane's mobility.  A wave whose surplus exceeds the list (`cap`, at
+// most kCoopCap) falls back to lane_choose for that ply.
+constexpr int kCoopCap = 64 * 8;  // overflow entries per wave per ply
 struct CoopWave {
     u64 rec[64][10];          // parent lane: P, O, its RunSets (8 words)
-    uint16_t list[kCoopCap];  // (parent lane << 8) | (parent plays White) << 6 | square
+    uint16_t list[kCoopCap];  // overflow: (parent lane << 8) | (parent plays White) << 6 | square
     u32 best[64];
-    u32 total;
+    u32 total, over, free;    // children, overflow entries, free rounds of the wave this ply
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -165,48 +175,74 @@ __device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, RunSet
 // w_s: the two eval tables (Black's, then White's, kEvalTable ints each)
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 side, const Position& pos, CoopWave& cw, const u64* rays,
-                           const int* w_s, u32 lane) {
+                           const int* w_s, u32 lane, u32 cap) {
+    const u32 white = side == OTH_WHITE ? 64u : 0u;
+    u32 cnt = 0;
     if (need) {
         u64* r = cw.rec[lane];
         r[0] = P;
         r[1] = O;
         *reinterpret_cast<RunSets*>(r + 2) = run_sets(pos);  // reversed once per parent, not per child
         cw.best[lane] = 0xFFFFFFFFu;
-        const u32 cnt = (u32)__popcll(pos.legal);
-        u32 off = atomicAdd(&cw.total, cnt);
-        if (off + cnt <= (u32)kCoopCap) {
-            const u32 tag = (lane << 8) | (side == OTH_WHITE ? 64u : 0u);
-            u64 m = pos.legal;
-            while (m) {
-                cw.list[off++] = (uint16_t)(tag | ((u32)__ffsll((unsigned long long)m) - 1u));
-                m &= m - 1;
-            }
-        }
+        cnt = (u32)__popcll(pos.legal);
+        atomicAdd(&cw.total, cnt);
     }
     wave_sync();
-    const u32 total = __builtin_amdgcn_readfirstlane(cw.total);
+    const u32 rounds = (__builtin_amdgcn_readfirstlane(cw.total) + 63u) >> 6;
+    u64 m = need ? pos.legal : 0ull;
+    const u32 own = min(cnt, rounds);
+    u32 free_base = 0;
+    if (cnt > rounds) {
+        // the surplus, highest squares first, goes to the overflow list
+        const u32 extra = cnt - rounds;
+        u32 off = atomicAdd(&cw.over, extra);
+        const bool fits = off + extra <= cap;
+        for (u32 i = 0; i < extra; i++) {
+            const u32 sq = 63u - (u32)__clzll((long long)m);
+            m ^= 1ull << sq;
+            if (fits) cw.list[off++] = (uint16_t)((lane << 8) | white | sq);
+        }
+    } else if (cnt < rounds) {
+        free_base = atomicAdd(&cw.free, rounds - cnt);
+    }
+    wave_sync();
+    const u32 over = __builtin_amdgcn_readfirstlane(cw.over);
     u32 result = 64;
-    if (total > (u32)kCoopCap) {
-        if (need) result = lane_choose<POLICY>(pos, P, O, rays, w_s + (side == OTH_WHITE ? kEvalTable : 0));
+    if (over > cap) {
+        if (need) result = lane_choose<POLICY>(pos, P, O, rays, w_s + (white ? kEvalTable : 0));
     } else {
-        const u32 rounds = (total + 63u) >> 6;
         for (u32 k = 0; k < rounds; k++) {
-            const u32 c = (k << 6) + lane;
-            if (c < total) {
-                const u32 e = cw.list[c];
-                const u32 par = e >> 8;
+            u32 par = lane, sq = 0, wt = white;
+            bool have = k < own;
+            if (have) {  // an own child: the lowest square left
+                sq = (u32)__ffsll((unsigned long long)m) - 1u;
+                m &= m - 1;
+            } else {  // a free round: the overflow entry of its number, if any
+                const u32 j = free_base + (k - own);
+                if (j < over) {
+                    const u32 e = cw.list[j];
+                    par = e >> 8;
+                    sq = e & 63u;
+                    wt = e & 64u;
+                    have = true;
+                }
+            }
+            if (have) {
                 u64 Pp, Op;
                 RunSets ps;
                 load_parent(cw.rec[par], Pp, Op, ps);
-                atomicMin(&cw.best[par],
-                          child_key<POLICY>(Pp, Op, ps, e & 63u, rays, w_s + ((e & 64u) ? kEvalTable : 0)));
+                atomicMin(&cw.best[par], child_key<POLICY>(Pp, Op, ps, sq, rays, w_s + (wt ? kEvalTable : 0)));
             }
         }
         wave_sync();
         if (need) result = cw.best[lane] & 63u;
     }
-    wave_sync();  // every lane has read total / best before the reset
-    if (lane == 0) cw.total = 0;
+    wave_sync();  // every lane has read the counters / best before the reset
+    if (lane == 0) {
+        cw.total = 0;
+        cw.over = 0;
+        cw.free = 0;
+    }
     wave_sync();
     return result;
 }
@@ -443,6 +479,7 @@ struct RolloutArgs {
     int64_t n;
     unsigned long long* work;  // the caller's work word (0 at start, left at 0)
     u64 last_ticket;           // 64 * (batches + waves - 1): the launch's last dequeue
+    u32 coop_cap;              // 1-ply policies: overflow list entries used (kCoopCap; tests lower it)
     EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table
 };
 
@@ -462,7 +499,11 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     __shared__ u64 rays[kTabRows * 64];
     __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
-    if (POLICY != OTH_POLICY_RANDOM && threadIdx.x < kBlock / 64) coop[threadIdx.x].total = 0;
+    if (POLICY != OTH_POLICY_RANDOM && threadIdx.x < kBlock / 64) {
+        coop[threadIdx.x].total = 0;
+        coop[threadIdx.x].over = 0;
+        coop[threadIdx.x].free = 0;
+    }
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
@@ -617,7 +658,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
                     const u32 c = coop_choose<POLICY>(choose, P, O, side, pos, coop[threadIdx.x >> 6], rays, w_s,
-                                                      (u32)lane);
+                                                      (u32)lane, a.coop_cap);
                     if (choose) sq = c;
                 }
                 if (moving) {
@@ -1395,6 +1436,9 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
     a.work = reinterpret_cast<unsigned long long*>(work);
+    // OTH_COOP_CAP (tests only) shrinks the cooperative overflow list, so the
+    // per-lane fallback of coop_choose runs from ordinary positions
+    a.coop_cap = (u32)std::min(std::max(env_int("OTH_COOP_CAP", kCoopCap), 0), kCoopCap);
     a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
     hipStream_t st = (hipStream_t)stream;
     if (policy == OTH_POLICY_EVAL) {

@@ -553,13 +553,18 @@ def _high_mobility_boards(m, seed, iters=400):
     return nb, cur
 
 
-def test_greedy_eval_coop_overflow_fallback_vs_oracle():
-    """A wave whose children overflow the cooperative list (64 x 20 entries)
-    falls back to per-lane evaluation for that ply (othello.hip coop_choose):
-    start every game where the mover has >= 21 legal moves (64 x 21 > 1280), so
-    the first plies of every wave take the fallback and later plies the
-    cooperative path."""
+@pytest.mark.parametrize("cap", [None, "64", "0"])
+def test_greedy_eval_coop_overflow_fallback_vs_oracle(cap, monkeypatch):
+    """The cooperative choice (othello.hip coop_choose) lists only the children
+    beyond a wave's R = ceil(T / 64) rounds; a wave whose surplus exceeds the
+    overflow list falls back to per-lane evaluation for that ply.  Start every
+    game where the mover has >= 21 legal moves (mobility far above the wave's
+    mean later on), and run with the full list, a 64-entry list (some plies
+    fall back) and an empty one (OTH_COOP_CAP=0: every ply with a surplus falls
+    back): all equal the oracle."""
     from subproc_amd.params import DEFAULT_WEIGHTS
+    if cap is not None:
+        monkeypatch.setenv("OTH_COOP_CAP", cap)
     nb, mob = _high_mobility_boards(4096, 12)
     assert mob.min() >= 21
     tt = np.full(len(nb), 1, np.uint8)

@@ -253,6 +253,38 @@ def test_every_code_all_densities_vs_oracle():
         assert (r.turn.cpu().numpy() == o["turn"]).all(), turn
 
 
+def test_mixed_side_codes_every_code_vs_oracle():
+    """Every lane its own side code -- Black, White, Empty (board.py's turn
+    after deserialize with a side string other than 'O'/'X') and codes no
+    square holds -- over boards of every density and every move code: the
+    step kernel's any-side path runs beside the fast path inside the same
+    waves, and legal/step/next-legal/turn/ret equal the oracle."""
+    rng = np.random.default_rng(17)
+    per = 512
+    parts = []
+    for k in (1, 2, 4):
+        occ = np.full(per, ~np.uint64(0), np.uint64)
+        for _ in range(k):
+            occ &= ~rng.integers(0, 2**64, per, dtype=np.uint64)
+        parts.append(~occ)
+    occ = np.concatenate(parts)
+    col = rng.integers(0, 2**64, len(occ), dtype=np.uint64)
+    black, white = occ & col, occ & ~col
+    n = len(occ) * 65
+    nb = np.repeat(np.stack([black, white], 1), 65, axis=0)
+    mv = np.tile(np.arange(65, dtype=np.uint8), len(occ))
+    tt = rng.choice(np.array([0, 1, 1, 2, 2, 3, 255], np.uint8), n)
+    boards = B(nb[:, 0], nb[:, 1])
+    assert (U(ops.legal(boards, T(tt))) == oracle.legal(nb, tt)).all()
+    r = ops.step(boards, T(tt), T(mv))
+    o = oracle.step(nb, tt, mv)
+    assert (U(r.flips) == o["flips"]).all()
+    assert (U(r.boards) == o["boards"]).all()
+    assert (U(r.legal_next) == o["legal_next"]).all()
+    assert (r.ret.cpu().numpy() == o["ret"]).all()
+    assert (r.turn.cpu().numpy() == o["turn"]).all()
+
+
 def test_rollout_random_65536_vs_oracle():
     n = 65536
     r = ops.rollout(n, 0x5EED, 0, device=DEV)

@@ -171,8 +171,9 @@ int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t
  * (0 <= p <= plies[i], plies capped at OTH_MOVES_STRIDE) goes to row
  * i*OTH_POS_STRIDE + p of pos_boards (rows, 2 x u64), pos_turn and pos_end
  * (is_game_over(), board.py:57-58; game_recorder.py:111).  start/start_turn
- * NULL = opening.  pos_turn / pos_end may be NULL; where given, their rows
- * past plies[i] are set to 0 (board rows past plies[i] are not written). */
+ * NULL = opening.  pos_turn / pos_end may be NULL.  Every row of a game's
+ * stride is written: rows past plies[i] are 0 in pos_boards, pos_turn and
+ * pos_end. */
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
                uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream);
 

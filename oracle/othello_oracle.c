@@ -461,8 +461,10 @@ int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_
         if (start) board_from_bits(&s, start[2 * i], start[2 * i + 1], start_turn ? start_turn[i] : Black);
         else board_init(&s);
         int np = plies[i] < MOVES_STRIDE ? plies[i] : MOVES_STRIDE;
-        /* rows past plies: turn and end 0 (include/othello.h oth_replay) */
+        /* rows past plies: board, turn and end 0 (include/othello.h oth_replay) */
         for (int p = np + 1; p <= MOVES_STRIDE; p++) {
+            pos[2 * (i * (MOVES_STRIDE + 1) + p)] = 0;
+            pos[2 * (i * (MOVES_STRIDE + 1) + p) + 1] = 0;
             if (pos_turn) pos_turn[i * (MOVES_STRIDE + 1) + p] = 0;
             if (pos_end) pos_end[i * (MOVES_STRIDE + 1) + p] = 0;
         }

@@ -837,10 +837,14 @@ __global__ __launch_bounds__(kBlock, 4) void replay_kernel(const u64* __restrict
 #pragma unroll
             for (int k = 0; k < kReplayBurst; k++) {
                 const int p = p0 + k;
+                b[k] = make_ulonglong2(0ull, 0ull);
                 if (p >= 0 && p <= np) {
                     b[k] = make_ulonglong2(bl, wh);
                     if (staged) {
-                        const u32 e = pos_end && moves_of(bl, wh) == 0 && moves_of(wh, bl) == 0;
+                        // is_game_over: White's moves only where Black has none (a
+                        // branch the waves skip mid-game; both ran for every position)
+                        u32 e = 0;
+                        if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
                         st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
                     }
                     // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
@@ -874,13 +878,20 @@ __global__ __launch_bounds__(kBlock, 4) void replay_kernel(const u64* __restrict
 #pragma unroll
             for (int k = 0; k < kReplayBurst; k++) {
                 const int p = p0 + k;
-                if (p >= 0 && p <= np) out[p] = b[k];
+                if (p >= 0 && p < OTH_POS_STRIDE) out[p] = b[k];
             }
             prev = cur;
 #pragma unroll
             for (int j = 0; j < OTH_MOVES_STRIDE / 8 - 1; j++) R[j] = R[j + 1];
             R[OTH_MOVES_STRIDE / 8 - 1] = 0;
             cur = R[0];
+        }
+        // the rest of the game's stride as 0, in the same line-filling bursts
+        // (every row is written: no separate fill pass over the output)
+        for (int p0 = -s + kReplayBurst * ((np + s) / kReplayBurst + 1); p0 < OTH_POS_STRIDE; p0 += kReplayBurst) {
+#pragma unroll
+            for (int k = 0; k < kReplayBurst; k++)
+                if (p0 + k < OTH_POS_STRIDE) out[p0 + k] = make_ulonglong2(0ull, 0ull);
         }
     }
     if (!staged) return;

@@ -273,8 +273,9 @@ def replay(moves, plies, start=None, start_turn=None):
     ps = _opt(start, "start", torch.int64, (n, 2), moves.device)
     pst = _opt(start_turn, "start_turn", torch.uint8, (n,), moves.device)
     dev = moves.device
-    b = torch.zeros((n, POS_STRIDE, 2), dtype=torch.int64, device=dev)
-    t = torch.empty((n, POS_STRIDE), dtype=torch.uint8, device=dev)  # rows past plies: written as 0
+    # every row is written by the kernel (rows past plies as 0): no fill pass
+    b = torch.empty((n, POS_STRIDE, 2), dtype=torch.int64, device=dev)
+    t = torch.empty((n, POS_STRIDE), dtype=torch.uint8, device=dev)
     e = torch.empty((n, POS_STRIDE), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
         check(_lib.load().oth_replay(ps, pst, pm, pp, b.data_ptr(), t.data_ptr(), e.data_ptr(), n, _stream()),

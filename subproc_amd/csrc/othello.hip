@@ -797,102 +797,127 @@ __device__ __forceinline__ void unstage_byte(u32 c, const uint8_t* start_turn, i
     e = (uint8_t)(c >> 7);
 }
 
-__global__ __launch_bounds__(kBlock, 4) void replay_kernel(const u64* __restrict__ start,
+// The bursts go out through a per-wave LDS exchange: after a lane has built
+// half a burst (4 rows = 64 B of one line), the wave's 64 half-lines are
+// stored by 4 lanes each, so a store instruction writes 16 half-lines of 64
+// contiguous bytes instead of 64 scattered 16-B rows.
+constexpr int kReplayBursts = (OTH_POS_STRIDE + 7 + kReplayBurst - 1) / kReplayBurst;  // 17 for every alignment
+constexpr int kXHalf = kReplayBurst / 2;  // rows per exchange
+
+__global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict__ start,
                                                         const uint8_t* __restrict__ start_turn,
                                                         const uint8_t* __restrict__ moves,
                                                         const uint8_t* __restrict__ plies, u64* __restrict__ pos,
                                                         uint8_t* __restrict__ pos_turn, uint8_t* __restrict__ pos_end,
                                                         int64_t n, int vec_moves, int vec_out) {
     extern __shared__ uint4 replay_stage4[];  // kReplayStage bytes when turn or end is wanted
+    __shared__ uint4 xrow[kBlock * kXHalf];   // lane-major: lane's 4 rows
+    __shared__ unsigned long long xaddr[kBlock];
+    __shared__ u32 xmask[kBlock];
     uint8_t* stage = reinterpret_cast<uint8_t*>(replay_stage4);
     const bool staged = pos_turn || pos_end;
     const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
     const int nb = (int)min<int64_t>(kBlock, n - blk0);
     const int lane = threadIdx.x;
+    const int wl = lane & 63, wbase = lane & ~63;
     if (staged) {
         for (int c = lane; c < kReplayStage / 16; c += kBlock) replay_stage4[c] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
-    if (lane < nb) {
-        const int64_t i = blk0 + lane;
-        u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
-        u32 t = OTH_BLACK;
-        if (start) {
-            const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(start)[i];
-            bl = s0.x;
-            wh = s0.y;
-            t = start_turn ? start_turn[i] : OTH_BLACK;
-        }
-        const int np = min<int>(plies[i], OTH_MOVES_STRIDE);
-        u64 R[OTH_MOVES_STRIDE / 8];
-        load_move_record(moves + i * OTH_MOVES_STRIDE, vec_moves != 0, R);
-        ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
-        uint8_t* st = stage + lane * OTH_POS_STRIDE;
-        const int s = (int)(i & 7);  // the first burst starts at p = -s: whole lines from there on
-        u64 prev = 0, cur = R[0];   // move-record words w[b-1], w[b] of burst b
-        for (int p0 = -s; p0 <= np; p0 += kReplayBurst) {
-            // move codes p0 .. p0+7 (bytes before position 0 are never used)
-            const u64 win = s ? (cur << (8 * s)) | (prev >> (64 - 8 * s)) : cur;
-            ulonglong2 b[kReplayBurst];
+    // every lane of a wave runs the 17 bursts (the exchange is wave-wide);
+    // a lane past the launch's last game has nothing valid to store
+    const bool live = lane < nb;
+    const int64_t i = blk0 + (live ? lane : 0);
+    u64 bl = OPEN_BLACK, wh = OPEN_WHITE;
+    u32 t = OTH_BLACK;
+    if (live && start) {
+        const ulonglong2 s0 = reinterpret_cast<const ulonglong2*>(start)[i];
+        bl = s0.x;
+        wh = s0.y;
+        t = start_turn ? start_turn[i] : OTH_BLACK;
+    }
+    const int np = live ? min<int>(plies[i], OTH_MOVES_STRIDE) : -1;
+    u64 R[OTH_MOVES_STRIDE / 8];
+    if (live) load_move_record(moves + i * OTH_MOVES_STRIDE, vec_moves != 0, R);
+    else
 #pragma unroll
-            for (int k = 0; k < kReplayBurst; k++) {
-                const int p = p0 + k;
-                b[k] = make_ulonglong2(0ull, 0ull);
-                if (p >= 0 && p <= np) {
-                    b[k] = make_ulonglong2(bl, wh);
-                    if (staged) {
-                        // is_game_over: White's moves only where Black has none (a
-                        // branch the waves skip mid-game; both ran for every position)
-                        u32 e = 0;
-                        if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
-                        st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
-                    }
-                    // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
-                    const u32 c = (u32)(win >> (8 * k)) & 0xffu;
-                    if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
-                        const StepOut o = put_s_any(bl, wh, t, c);  // side Empty / none (rare)
-                        bl = o.bl;
-                        wh = o.wh;
-                        t = o.t;
-                    } else if (p < np) {
-                        if (c == OTH_PASS) {
-                            t ^= 3u;
-                        } else if (c < 64) {
-                            const bool black = t == OTH_BLACK;
-                            u64 P = black ? bl : wh, O = black ? wh : bl;
-                            const u64 mm = 1ull << c;
-                            if (!((P | O) & mm)) {
-                                const u64 f = flips_carry(c, P, O);
-                                if (f) {
-                                    P |= f | mm;
-                                    O = andn(O, f);
-                                    bl = black ? P : O;
-                                    wh = black ? O : P;
-                                    t ^= 3u;
-                                }
+        for (int j = 0; j < OTH_MOVES_STRIDE / 8; j++) R[j] = 0;
+    ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
+    uint8_t* st = stage + lane * OTH_POS_STRIDE;
+    const int s = (int)(i & 7);  // the first burst starts at p = -s: whole lines from there on
+    u64 prev = 0, cur = R[0];   // move-record words w[b-1], w[b] of burst b
+    for (int bi = 0; bi < kReplayBursts; bi++) {
+        const int p0 = 8 * bi - s;
+        // move codes p0 .. p0+7 (bytes before position 0 are never used)
+        const u64 win = s ? (cur << (8 * s)) | (prev >> (64 - 8 * s)) : cur;
+        ulonglong2 b[kReplayBurst];
+#pragma unroll
+        for (int k = 0; k < kReplayBurst; k++) {
+            const int p = p0 + k;
+            b[k] = make_ulonglong2(0ull, 0ull);  // rows past plies are 0
+            if (p >= 0 && p <= np) {
+                b[k] = make_ulonglong2(bl, wh);
+                if (staged) {
+                    // is_game_over: White's moves only where Black has none (a
+                    // branch the waves skip mid-game)
+                    u32 e = 0;
+                    if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
+                    st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
+                }
+                // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
+                const u32 c = (u32)(win >> (8 * k)) & 0xffu;
+                if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
+                    const StepOut o = put_s_any(bl, wh, t, c);  // side Empty / none (rare)
+                    bl = o.bl;
+                    wh = o.wh;
+                    t = o.t;
+                } else if (p < np) {
+                    if (c == OTH_PASS) {
+                        t ^= 3u;
+                    } else if (c < 64) {
+                        const bool black = t == OTH_BLACK;
+                        u64 P = black ? bl : wh, O = black ? wh : bl;
+                        const u64 mm = 1ull << c;
+                        if (!((P | O) & mm)) {
+                            const u64 f = flips_carry(c, P, O);
+                            if (f) {
+                                P |= f | mm;
+                                O = andn(O, f);
+                                bl = black ? P : O;
+                                wh = black ? O : P;
+                                t ^= 3u;
                             }
                         }
                     }
                 }
             }
+        }
 #pragma unroll
-            for (int k = 0; k < kReplayBurst; k++) {
-                const int p = p0 + k;
-                if (p >= 0 && p < OTH_POS_STRIDE) out[p] = b[k];
+        for (int h = 0; h < kReplayBurst / kXHalf; h++) {
+            u32 valid = 0;
+#pragma unroll
+            for (int k = 0; k < kXHalf; k++) {
+                const int p = p0 + h * kXHalf + k;
+                const ulonglong2 v = b[h * kXHalf + k];
+                xrow[lane * kXHalf + k] = make_uint4((u32)v.x, (u32)(v.x >> 32), (u32)v.y, (u32)(v.y >> 32));
+                valid |= (live && p >= 0 && p < OTH_POS_STRIDE ? 1u : 0u) << k;
             }
-            prev = cur;
+            xaddr[lane] = reinterpret_cast<unsigned long long>(out + (p0 + h * kXHalf));
+            xmask[lane] = valid;
+            wave_sync();
 #pragma unroll
-            for (int j = 0; j < OTH_MOVES_STRIDE / 8 - 1; j++) R[j] = R[j + 1];
-            R[OTH_MOVES_STRIDE / 8 - 1] = 0;
-            cur = R[0];
+            for (int j = 0; j < 64 / (64 / kXHalf); j++) {
+                const int src = wbase + j * (64 / kXHalf) + wl / kXHalf, c = wl % kXHalf;
+                if (xmask[src] >> c & 1u)
+                    reinterpret_cast<uint4*>(xaddr[src])[c] = xrow[src * kXHalf + c];
+            }
+            wave_sync();  // the wave has read this half before the next overwrites it
         }
-        // the rest of the game's stride as 0, in the same line-filling bursts
-        // (every row is written: no separate fill pass over the output)
-        for (int p0 = -s + kReplayBurst * ((np + s) / kReplayBurst + 1); p0 < OTH_POS_STRIDE; p0 += kReplayBurst) {
+        prev = cur;
 #pragma unroll
-            for (int k = 0; k < kReplayBurst; k++)
-                if (p0 + k < OTH_POS_STRIDE) out[p0 + k] = make_ulonglong2(0ull, 0ull);
-        }
+        for (int j = 0; j < OTH_MOVES_STRIDE / 8 - 1; j++) R[j] = R[j + 1];
+        R[OTH_MOVES_STRIDE / 8 - 1] = 0;
+        cur = R[0];
     }
     if (!staged) return;
     __syncthreads();

@@ -411,6 +411,17 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
             fl.data_ptr(), ln.data_ptr(), rt.data_ptr(), None, n, stream.cuda_stream)
     for _ in range(max(3, args.warmup)):
         _lib.check(lib.oth_step(*ptrs), "oth_step")
+    if n >= 1 << 20:
+        # the steady-state line: ~200 ms more of untimed launches, so the clock
+        # has ramped back up after the launch-bound lines before it (10
+        # warmup launches of 16M boards are 2 ms; timed that way the step ran
+        # 10-13% slower than after a ramp, tools/diag/step_ab.py)
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < 0.2:
+            for _ in range(20):
+                _lib.check(lib.oth_step(*ptrs), "oth_step")
+            torch.cuda.synchronize()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()

@@ -372,11 +372,16 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
         t_out = o.t;
         if (legal_next) lg = legal_any(nb, nw, t_out);
     }
-    if (legal_next) legal_next[i] = lg;
-    if (boards_out) reinterpret_cast<ulonglong2*>(boards_out)[i] = make_ulonglong2(nb, nw);
-    if (turn_out) turn_out[i] = (uint8_t)t_out;
-    if (flips_out) flips_out[i] = f;
-    if (ret_out) ret_out[i] = (int8_t)r;
+    // streaming outputs: non-temporal stores (tools/diag/step_ab.py at 16M
+    // boards: 157 against 161 us with ordinary stores)
+    if (legal_next) __builtin_nontemporal_store(lg, legal_next + i);
+    if (boards_out) {
+        __builtin_nontemporal_store(nb, boards_out + 2 * i);
+        __builtin_nontemporal_store(nw, boards_out + 2 * i + 1);
+    }
+    if (turn_out) __builtin_nontemporal_store((uint8_t)t_out, turn_out + i);
+    if (flips_out) __builtin_nontemporal_store(f, flips_out + i);
+    if (ret_out) __builtin_nontemporal_store((int8_t)r, ret_out + i);
     if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1);
 }
 

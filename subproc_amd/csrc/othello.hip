@@ -970,40 +970,82 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
     }
 }
 
-// serialize_str (board.py:214-243) + '\n' of record r = 67 bytes.  One thread
-// writes 16 bytes of the concatenated text, so stores are aligned dwordx4.
+// serialize_str (board.py:214-243) + '\n' of record r = 67 bytes: 64 squares
+// row-major ('O' black, 'X' white, '-' empty), ' ', the side ('O' / 'X' /
+// '-'), '\n'.  One lane per line: a rank of 8 squares becomes 8 characters
+// at once from a byte-expansion table (byte k of kExpand[b] is 0xFF iff bit k
+// of b is set), and the wave's 64 lines (4,288 contiguous bytes) are
+// assembled in LDS -- each lane ORs its line in at its byte offset, the two
+// dwords it shares with its neighbours included -- and stored by the whole
+// wave as aligned 16-byte chunks.  (The first version had every lane build
+// 16 bytes of text character by character, ~8 VALU each: 1.85 TB/s.)
 constexpr int kLine = 67;
-__device__ __forceinline__ uint8_t book_char(u64 bl, u64 wh, u32 t, u32 col) {
-    if (col < 64) return (bl >> col & 1) ? 'O' : ((wh >> col & 1) ? 'X' : '-');
-    if (col == 64) return ' ';
-    if (col == 65) return t == OTH_BLACK ? 'O' : (t == OTH_WHITE ? 'X' : '-');
-    return '\n';
+constexpr int kBookWave = 64 * kLine;  // 4,288 = 268 x 16 bytes
+__device__ __forceinline__ u64 rank_chars(u64 bl, u64 wh, u32 rank, const u64* ex) {
+    const u64 mb = ex[(u32)(bl >> (8 * rank)) & 0xFFu], mw = ex[(u32)(wh >> (8 * rank)) & 0xFFu];
+    // '-' ^ ('O' ^ '-') on Black squares ^ ('X' ^ '-') on White ones
+    return 0x2D2D2D2D2D2D2D2Dull ^ (mb & 0x6262626262626262ull) ^ (mw & 0x7575757575757575ull);
 }
 __global__ __launch_bounds__(kBlock) void book_text_kernel(const u64* __restrict__ boards,
                                                            const uint8_t* __restrict__ turn, int64_t n,
                                                            uint8_t* __restrict__ out) {
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t total = n * kLine;
-    const int64_t k0 = j * 16;
-    if (k0 >= total) return;
-    const int64_t r0 = k0 / kLine;
-    const int64_t r1 = min<int64_t>(r0 + 1, n - 1);
-    const ulonglong2 b0 = reinterpret_cast<const ulonglong2*>(boards)[r0];
-    const ulonglong2 b1 = reinterpret_cast<const ulonglong2*>(boards)[r1];
-    const u32 t0 = turn[r0], t1 = turn[r1];
-    const u32 c0 = (u32)(k0 - r0 * kLine);
-    u32 w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const u32 col = c0 + q;
-        const bool second = col >= kLine;
-        const uint8_t ch = second ? book_char(b1.x, b1.y, t1, col - kLine) : book_char(b0.x, b0.y, t0, col);
-        w[q >> 2] |= (u32)ch << (8 * (q & 3));
+    __shared__ u64 ex[256];
+    __shared__ u32 stage_all[(kBlock / 64) * (kBookWave / 4)];
+    for (int e = threadIdx.x; e < 256; e += kBlock) {
+        u64 m = 0;
+        for (int k = 0; k < 8; k++)
+            if (e >> k & 1) m |= 0xFFull << (8 * k);
+        ex[e] = m;
     }
-    if (k0 + 16 <= total) {
-        *reinterpret_cast<uint4*>(out + k0) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-        for (int q = 0; k0 + q < total; q++) out[k0 + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32* st = stage_all + wv * (kBookWave / 4);
+    for (int d = wl; d < kBookWave / 4; d += 64) st[d] = 0;
+    __syncthreads();
+    const int64_t line0 = ((int64_t)blockIdx.x * (kBlock / 64) + wv) * 64;  // the wave's first line
+    const int64_t li = line0 + wl;
+    if (li < n) {
+        const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards)[li];
+        const u32 t = turn[li];
+        // the line as 17 dwords (the 17th: ' ', side, '\n')
+        u32 L[18];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u64 w = rank_chars(b.x, b.y, (u32)r, ex);
+            L[2 * r] = (u32)w;
+            L[2 * r + 1] = (u32)(w >> 32);
+        }
+        const u32 side = t == OTH_BLACK ? 'O' : (t == OTH_WHITE ? 'X' : '-');
+        L[16] = 0x20u | (side << 8) | (0x0Au << 16);
+        L[17] = 0;
+        // byte offset 67 * wl = 4 * d0 + phi: dword k of the shifted line is
+        // bytes [4k - phi, 4k - phi + 4) of the line
+        const u32 o = (u32)wl * kLine, d0 = o >> 2, sh = 8u * (o & 3u);
+        u32 lo = 0;
+#pragma unroll
+        for (int k = 0; k < 18; k++) {
+            const u32 v = (u32)((((u64)L[k] << 32) | lo) >> (32 - sh));
+            lo = L[k];
+            // the first and the last dword are shared with the neighbouring
+            // lines (bytes outside this line are 0 here): OR them in
+            if (k == 0 || k >= 16) {
+                if (v) atomicOr(&st[d0 + k], v);
+            } else {
+                st[d0 + k] = v;
+            }
+        }
+    }
+    wave_sync();
+    const int64_t bytes = (min<int64_t>(n, line0 + 64) - line0) * kLine;
+    if (bytes <= 0) return;
+    uint8_t* dst = out + line0 * kLine;  // line0 * 67 is a multiple of 16 (line0 is of 64)
+    for (int c = wl; c * 16 < bytes; c += 64) {
+        const uint4 v = reinterpret_cast<const uint4*>(st)[c];
+        if (c * 16 + 16 <= bytes) {
+            *reinterpret_cast<uint4*>(dst + c * 16) = v;
+        } else {  // the launch's last partial chunk
+            const u32 w[4] = {v.x, v.y, v.z, v.w};
+            for (int q = 0; c * 16 + q < bytes; q++) dst[c * 16 + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+        }
     }
 }
 
@@ -1539,9 +1581,8 @@ int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* 
 int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream) {
     if (n < 0 || (n > 0 && (!boards || !turn || !out))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    const int64_t threads = (n * kLine + 15) / 16;
-    book_text_kernel<<<blocks_for(threads), kBlock, 0, (hipStream_t)stream>>>(boards, turn, n,
-                                                                             reinterpret_cast<uint8_t*>(out));
+    book_text_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards, turn, n,
+                                                                       reinterpret_cast<uint8_t*>(out));
     return launched();
 }
 

@@ -202,14 +202,13 @@ def test_books_features_eval_pair():
     outs = [None, None, Buf(np.zeros(n, np.uint8)), Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8)), None]
     both("oth_rollout", None, None, 5, 0, 0, 0, None, None, outs[2], outs[3], None, work(), n)
     same(outs[2], outs[3])
-    pos = Buf(np.zeros((n, _lib.POS_STRIDE, 2), np.uint64))
+    pos = Buf(np.full((n, _lib.POS_STRIDE, 2), 0x5A5A5A5A5A5A5A5A, np.uint64))
     pt, pe = Buf(np.full((n, _lib.POS_STRIDE), 0xAB, np.uint8)), Buf(np.full((n, _lib.POS_STRIDE), 0xCD, np.uint8))
     both("oth_replay", None, None, outs[3], outs[2], pos, pt, pe, n)
-    # board rows past plies are left untouched by both (zero-initialised here);
-    # turn / end rows past plies are written as 0 by both
+    # every row is written by both: board, turn and end rows past plies as 0
     same(pos, pt, pe)
     past = np.arange(_lib.POS_STRIDE)[None, :] > outs[2].h[:, None]
-    assert (pt.h[past] == 0).all() and (pe.h[past] == 0).all()
+    assert (pos.h[past] == 0).all() and (pt.h[past] == 0).all() and (pe.h[past] == 0).all()
     k = n * _lib.POS_STRIDE
     flat_b = Buf(pos.h.reshape(k, 2))
     flat_t = Buf(pt.h.reshape(k))

@@ -76,3 +76,19 @@ def test_book_text_tail_lengths():
         b, t, _ = ops.reset(n, "cuda")
         txt = ops.book_text(b, t).cpu().numpy().tobytes().decode()
         assert txt == "---------------------------XO------OX--------------------------- O\n" * n
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 1000])
+def test_book_text_random_boards_every_side(n):
+    """Arbitrary boards (any occupancy) and side codes 0..3 at ragged sizes --
+    lines that share dwords with their neighbours in the kernel's LDS
+    assembly, and waves with fewer than 64 lines -- against the host codec."""
+    from subproc_amd import codec
+    rng = np.random.default_rng(n)
+    occ = rng.integers(0, 2**64, n, dtype=np.uint64)
+    col = rng.integers(0, 2**64, n, dtype=np.uint64)
+    nb = np.stack([occ & col, occ & ~col], 1)
+    side = rng.integers(0, 4, n).astype(np.uint8)
+    txt = ops.book_text(ops.from_numpy_u64(nb, "cuda"), torch.as_tensor(side).cuda()).cpu().numpy().tobytes().decode()
+    want = "".join(codec.serialize_str(int(b), int(w), int(t)) + "\n" for (b, w), t in zip(nb, side))
+    assert txt == want

@@ -92,3 +92,28 @@ def test_book_text_random_boards_every_side(n):
     txt = ops.book_text(ops.from_numpy_u64(nb, "cuda"), torch.as_tensor(side).cuda()).cpu().numpy().tobytes().decode()
     want = "".join(codec.serialize_str(int(b), int(w), int(t)) + "\n" for (b, w), t in zip(nb, side))
     assert txt == want
+
+
+def test_book_text_and_features_unaligned_outputs():
+    """Outputs that are not 16-byte aligned (a caller's buffer + 1): the kernels
+    assemble each wave's bytes in LDS and fall back to byte stores; the bytes
+    equal the aligned call's."""
+    from subproc_amd import _lib
+    n = 300
+    rng = np.random.default_rng(5)
+    occ = rng.integers(0, 2**64, n, dtype=np.uint64)
+    col = rng.integers(0, 2**64, n, dtype=np.uint64)
+    nb = np.stack([occ & col, occ & ~col], 1)
+    side = torch.as_tensor(rng.integers(0, 4, n).astype(np.uint8)).cuda()
+    b = ops.from_numpy_u64(nb, "cuda")
+    L = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    want_txt = ops.book_text(b, side)
+    buf = torch.zeros(n * 67 + 32, dtype=torch.uint8, device="cuda")
+    assert L.oth_book_text(b.data_ptr(), side.data_ptr(), n, buf.data_ptr() + 1, st) == 0
+    assert torch.equal(buf[1:1 + n * 67], want_txt) and int(buf[0]) == 0 and int(buf[1 + n * 67]) == 0
+    fs = torch.clamp(side, 1, 2)
+    want_f = ops.features(b, fs).reshape(-1)
+    buf = torch.zeros(n * 10 + 32, dtype=torch.uint8, device="cuda")
+    assert L.oth_features(b.data_ptr(), fs.data_ptr(), buf.data_ptr() + 3, n, st) == 0
+    assert torch.equal(buf[3:3 + n * 10], want_f) and int(buf[3 + n * 10]) == 0

@@ -117,3 +117,30 @@ def test_book_text_and_features_unaligned_outputs():
     buf = torch.zeros(n * 10 + 32, dtype=torch.uint8, device="cuda")
     assert L.oth_features(b.data_ptr(), fs.data_ptr(), buf.data_ptr() + 3, n, st) == 0
     assert torch.equal(buf[3:3 + n * 10], want_f) and int(buf[3 + n * 10]) == 0
+
+
+def test_replay_full_size_properties():
+    """262,144 games (the TD batch and the book-emitter bench size) replayed
+    in one launch: every row of every game's stride checked by size-independent
+    properties on the device (rows past plies 0; the last recorded position is
+    the rollout's final board and the only one with is_game_over; the side to
+    move at row p+1 is the one put_s left), and a strided sample of games --
+    the last ones included -- against the oracle's mailbox replay."""
+    n = 1 << 18
+    r = ops.rollout(n, 77, 1 << 30, record_moves=True, device="cuda")
+    pos = ops.replay(r.moves, r.plies)
+    pl = r.plies.long()
+    rows = torch.arange(129, device="cuda")[None, :]
+    inside = rows <= pl[:, None]
+    assert bool((pos.boards[~inside] == 0).all()) and bool((pos.turn[~inside] == 0).all())
+    assert bool((pos.end[~inside] == 0).all())
+    last = pos.boards[torch.arange(n, device="cuda"), pl]
+    assert torch.equal(last, r.final_boards)
+    ends = pos.end.long().sum(1)
+    assert bool((ends == 1).all()) and bool((pos.end[torch.arange(n, device="cuda"), pl] == 1).all())
+    assert bool(((pos.turn == 1) | (pos.turn == 2))[inside].all())
+    idx = np.unique(np.concatenate([np.arange(0, n, 1021), np.arange(n - 64, n)]))
+    o = oracle.replay(r.moves.cpu().numpy()[idx], r.plies.cpu().numpy()[idx])
+    np.testing.assert_array_equal(U(pos.boards[idx].reshape(-1, 2)).reshape(len(idx), 129, 2), o["boards"])
+    np.testing.assert_array_equal(pos.turn[idx].cpu().numpy(), o["turn"])
+    np.testing.assert_array_equal(pos.end[idx].cpu().numpy(), o["end"])

@@ -21,6 +21,7 @@ Also reported on rank 0 (secondary, same JSON line):
   * eval       : 1,048,576 games of the 1-ply linear-eval policy with the
     learner's default weights (SURVEY.md §8f row 2);
   * td_state_map: the learner's TD state-map update for 262,144 GPU games;
+  * book_emitter: replay and serialize_str text of 262,144 games (§8f row 1);
   * cpu_baseline: the C oracle (mailbox restatement of board.py) on a bounded
     sample of the same workload on the host cores.
 
@@ -205,6 +206,7 @@ def main():
             guarded("greedy_1M", lambda: policy_line("greedy"))
         guarded("eval_1M", lambda: policy_line("eval"))
         guarded("td_state_map", lambda: _bench_td(ops, torch, dev, args))
+        guarded("book_emitter", lambda: _bench_books(ops, torch, dev, args))
         out["secondary"] = sec
         try:
             out["cpu_baseline"] = _cpu_baseline(args, policy if args.workload != "step" else "step")
@@ -493,6 +495,39 @@ def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):
     dt = time.perf_counter() - t0
     return {"metric": "env-steps/sec (random self-play, 16M games per launch)", "value": int(hist[132]) / dt,
             "unit": "env-steps/s", "games": games, "launches": reps, "ms_per_launch": dt / reps * 1e3}
+
+
+def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
+    """§8f row 1: the book emitter over 262,144 games -- oth_replay (every
+    recorded position, turn and is_game_over) and oth_book_text of all
+    262,144 x 129 rows; HIP events, after 3 untimed launches each."""
+    r = ops.rollout(games, args.seed, 1 << 40, "random", record_moves=True, device=dev)
+    out = {}
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    us = timed(lambda: ops.replay(r.moves, r.plies))
+    rows = games * 129
+    # algorithmic bytes: 128-B move record + plies read; 129 rows x (16 + 1 + 1) written
+    rb = games * (128 + 1 + 129 * 18)
+    out["replay"] = {"games": games, "us": us, "achieved_gbs": rb / us / 1e3, "frac_hbm": rb / us / 1e3 / HBM_PEAK_GBS}
+    pos = ops.replay(r.moves, r.plies)
+    b, t = pos.boards.reshape(-1, 2), pos.turn.reshape(-1)
+    us = timed(lambda: ops.book_text(b, t))
+    tb = rows * (16 + 1 + 67)
+    out["book_text"] = {"lines": rows, "us": us, "achieved_gbs": tb / us / 1e3, "frac_hbm": tb / us / 1e3 / HBM_PEAK_GBS}
+    out["metric"] = "book emitter (replay + serialize_str text) per 262,144 games"
+    return out
 
 
 def _bench_td(ops, torch, dev, args, games=1 << 18):

@@ -862,16 +862,42 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
             b[k] = make_ulonglong2(0ull, 0ull);  // rows past plies are 0
             if (p >= 0 && p <= np) {
                 b[k] = make_ulonglong2(bl, wh);
+                const u32 c = (u32)(win >> (8 * k)) & 0xffu;
+                const bool fast = t == OTH_BLACK || t == OTH_WHITE;
+                if (pos_end && fast) {
+                    // one analysis of the mover serves is_game_over (the other
+                    // side is analysed only where the mover has no move) and the
+                    // flips of its move (run sets and the move's rays, in registers)
+                    const bool black = t == OTH_BLACK;
+                    u64 P = black ? bl : wh, O = black ? wh : bl;
+                    Position pm;
+                    analyse(P, O, pm);
+                    u32 e = 0;
+                    if (pm.legal == 0) e = moves_of(O, P) == 0;
+                    st[p] = (uint8_t)(t | (e << 7));
+                    if (p < np) {
+                        if (c == OTH_PASS) {
+                            t ^= 3u;
+                        } else if (c < 64 && !((P | O) >> c & 1ull)) {
+                            const u64 f = flips_runs(c, run_sets(pm));
+                            if (f) {
+                                P = or3(P, f, 1ull << c);
+                                O = andn(O, f);
+                                bl = black ? P : O;
+                                wh = black ? O : P;
+                                t ^= 3u;
+                            }
+                        }
+                    }
+                    continue;
+                }
                 if (staged) {
-                    // is_game_over: White's moves only where Black has none (a
-                    // branch the waves skip mid-game)
                     u32 e = 0;
                     if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
                     st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
                 }
                 // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
-                const u32 c = (u32)(win >> (8 * k)) & 0xffu;
-                if (p < np && t != OTH_BLACK && t != OTH_WHITE) {
+                if (p < np && !fast) {
                     const StepOut o = put_s_any(bl, wh, t, c);  // side Empty / none (rare)
                     bl = o.bl;
                     wh = o.wh;

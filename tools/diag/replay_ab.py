@@ -17,7 +17,7 @@ for p in sys.argv[1:]:
     L = ctypes.CDLL(os.path.abspath(p))
     L.oth_replay.restype, L.oth_replay.argtypes = res, argt
     libs.append((os.path.basename(p), L))
-n = 1 << 18
+n = int(os.environ.get("REPLAY_N", 1 << 18))
 r = ops.rollout(n, 7, 0, "random", record_moves=True, device="cuda")
 b = torch.empty((n, 129, 2), dtype=torch.int64, device="cuda")
 t = torch.empty((n, 129), dtype=torch.uint8, device="cuda")

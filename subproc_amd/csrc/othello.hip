@@ -1425,6 +1425,7 @@ inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
 // tools/diag only: OTH_ROLLOUT_BLOCKS_PER_CU.
 struct Tuning {
     unsigned resident_blocks[3];  // per policy
+    unsigned random_big_blocks;   // the random policy at >= kBigLaunch games
 };
 
 int env_int(const char* name, int dflt) {
@@ -1436,6 +1437,8 @@ int env_int(const char* name, int dflt) {
 // first use; the only state the library keeps, and none of it on the device
 constexpr int kMaxDevices = 64;
 constexpr int kMaxBlocksPerCu = 5;
+constexpr int kRandomBlocksPerCu = 3;
+constexpr int64_t kBigLaunch = 1 << 22;  // games: a launch this large amortises its own tail
 struct DeviceState {
     std::atomic<int> ready{0};
     Tuning tuning;
@@ -1459,12 +1462,24 @@ DeviceState* device_state() {
         for (int p = 0; p < 3; p++) {
             int per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[p], kBlock, 0);
-            // 5 blocks of 4 waves per CU (5 waves/SIMD) measured fastest for the
-            // VALU-bound loop (tools/diag/sweep_rollout.sh: 0.471 ms vs 0.484-0.500 at
-            // 6-8); more waves only add batch-tail idle lanes
-            per_cu = per_cu > 0 ? std::min(per_cu, kMaxBlocksPerCu) : 2;
+            // the random policy: 3 blocks of 4 waves per CU, so that two launches
+            // in flight (2 streams, as INTEGRATION.md advises) are resident side
+            // by side (6 of the 7 waves/SIMD its 70 VGPRs allow): 1.97e11
+            // env-steps/s against 1.92e11 at 5 and 1.94e11 at 4 (tools/diag/bpc_k.sh,
+            // 1M games per launch, 100 timed steps; 1.85-1.89e11 against
+            // 1.83-1.84e11 at 20).  A launch of >= kBigLaunch games keeps 5: it
+            // runs alone for most of its life (16M games, one stream: 2.0e11 at 5,
+            // 1.91e11 at 3).  The 1-ply policies keep <= 5 (tools/diag/sweep_rollout.sh:
+            // more waves only add batch-tail idle lanes)
+            const int occ = per_cu;
+            const int cap = p == OTH_POLICY_RANDOM ? kRandomBlocksPerCu : kMaxBlocksPerCu;
+            per_cu = occ > 0 ? std::min(occ, cap) : 2;
             per_cu = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", per_cu);
             d.tuning.resident_blocks[p] = (unsigned)(cus * per_cu);
+            if (p == OTH_POLICY_RANDOM) {
+                const int big = env_int("OTH_ROLLOUT_BLOCKS_PER_CU", occ > 0 ? std::min(occ, kMaxBlocksPerCu) : 2);
+                d.tuning.random_big_blocks = (unsigned)(cus * big);
+            }
         }
         d.ready.store(1, std::memory_order_release);
     }
@@ -1546,7 +1561,9 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     if (!ds) return status(hipErrorInvalidDevice);
     const Tuning& t = ds->tuning;
     const int64_t max_blocks = (n + kBlock - 1) / kBlock;
-    const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)t.resident_blocks[policy]);
+    const unsigned resident =
+        policy == OTH_POLICY_RANDOM && n >= kBigLaunch ? t.random_big_blocks : t.resident_blocks[policy];
+    const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)resident);
     a.work = reinterpret_cast<unsigned long long*>(work);
     // OTH_COOP_CAP (tests only) shrinks the cooperative overflow list, so the
     // per-lane fallback of coop_choose runs from ordinary positions

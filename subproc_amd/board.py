@@ -31,6 +31,7 @@ values, the side to move and the ply counter on the host, plus the text
 codecs.  For throughput use :class:`subproc_amd.env.VecEnv` / :mod:`subproc_amd.ops`.
 """
 import operator
+import threading
 
 import numpy as np
 
@@ -189,14 +190,17 @@ class _Device:
         return out.cpu().tolist()[:n]
 
 
-_DEV = None
+_TLS = threading.local()
 
 
 def _device():
-    global _DEV
-    if _DEV is None:
-        _DEV = _Device()
-    return _DEV
+    """This thread's _Device: every call stages through the object's pinned and
+    device buffers between its launch and its fetch, so Boards used from
+    several threads each get their own (reference Boards share no state)."""
+    d = getattr(_TLS, "dev", None)
+    if d is None:
+        d = _TLS.dev = _Device()
+    return d
 
 
 def _index(i):

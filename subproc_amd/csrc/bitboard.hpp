@@ -216,6 +216,11 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
 // the move's bit from the table (row kRayRows)
 __device__ __forceinline__ u64 square_bit(u32 sq, const u64* tab) { return tab[kRayRows * 64 + sq]; }
 __device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bitop3<0x80>(a, b, c); }
+// For a ray R leaving the move in increasing bit order and the run set A of
+// the opposite direction, the flipped discs are the squares of R before R's
+// first square that is not in A: with x = R & ~A, R & A & (x - 1).  (x - 1)
+// sets the bits below x's lowest bit but keeps x's higher bits, so the "& A"
+// is needed.
 __device__ __forceinline__ u64 run_prefix(u64 R, u64 A) {
     const u64 x = andn(R, A);
     return and3(R, A, dec64(x));
@@ -233,20 +238,43 @@ __device__ __forceinline__ RunSets run_sets(const Position& s) {
     return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), rev64(s.A[2]), rev64(s.A[4]), rev64(s.A[6])};
 }
 
-// flips of the move at square sq (bit mv).  Horizontal: the run of A[1] that
-// starts right east of the move is exactly its east flips (an A[1] run is
-// attached to a P disc on its far side and bounded by the empty move square on
-// this side; A runs lie on the inner files, so the carry never leaves the
-// row): one add, as east_run.  West the same on the reversed board with A[0].
-// The other six by the ray tables (run_prefix).
-__device__ __forceinline__ u64 flips_rays(u32 sq, u64 mv, const RunSets& r, const u64* tab) {
-    u64 f = east_run(mv, r.A1);
-    u64 fr = east_run(tab[(kRayRows + 1) * 64 + sq], r.rA0);  // west, in reversed space (rev64(mv))
-    f = or3(f, run_prefix(tab[0 * 64 + sq], r.A3), run_prefix(tab[1 * 64 + sq], r.A5));
-    f |= run_prefix(tab[2 * 64 + sq], r.A7);
-    fr = or3(fr, run_prefix(tab[3 * 64 + sq], r.rA2), run_prefix(tab[4 * 64 + sq], r.rA4));
-    fr |= run_prefix(tab[5 * 64 + sq], r.rA6);
-    return f | rev64(fr);
+// The flips of the move at square sq (bit mv) in two parts, both including
+// the move's own bit: f in the normal orientation (east and the rays leaving
+// in increasing bit order) and fr for the rays leaving in decreasing order,
+// computed on the bit-reversed board and reversed back once.  Horizontal: the
+// run of A[1] that starts right east of the move is exactly its east flips
+// (an A[1] run is attached to a P disc on its far side and bounded by the
+// empty move square on this side; A runs lie on the inner files, so the carry
+// never leaves the row): one add, as east_run, and the move's bit ORed in by
+// the same v_bitop3_b32.  West the same on the reversed board with A[0].  The
+// other six by the ray tables (run_prefix).  place() applies both parts: the
+// move's bit is never an opponent disc, so carrying it in the flips costs
+// nothing and saves the apply's separate OR.
+struct Flips {
+    u64 f, fr;
+};
+// col = tab + sq: the move's column of the table (rows 64 entries apart)
+__device__ __forceinline__ Flips flips_col(u64 mv, const RunSets& r, const u64* col) {
+    const u64 rmv = col[(kRayRows + 1) * 64];
+    u64 f = bitop3<0xBA>(r.A1, lshl1_add(mv, r.A1), mv);     // (A1 & ~(A1 + (mv << 1))) | mv
+    u64 fr = bitop3<0xBA>(r.rA0, lshl1_add(rmv, r.rA0), rmv);  // west, in reversed space
+    f = or3(f, run_prefix(col[0 * 64], r.A3), run_prefix(col[1 * 64], r.A5));
+    f |= run_prefix(col[2 * 64], r.A7);
+    fr = or3(fr, run_prefix(col[3 * 64], r.rA2), run_prefix(col[4 * 64], r.rA4));
+    fr |= run_prefix(col[5 * 64], r.rA6);
+    return Flips{f, rev64(fr)};
+}
+__device__ __forceinline__ Flips flips_rays(u32 sq, const RunSets& r, const u64* tab) {
+    return flips_col(tab[kRayRows * 64 + sq], r, tab + sq);
+}
+// the move: mover X |= flips | mv, opponent Y &= ~flips
+__device__ __forceinline__ void place(u64& X, u64& Y, const Flips& fl) {
+    X = or3(X, fl.f, fl.fr);
+    Y = bitop3<0x10>(Y, fl.f, fl.fr);  // Y & ~f & ~fr
+}
+// the column of the square whose byte offset kth_bit_off returned
+__device__ __forceinline__ const u64* ray_col(const u64* tab, u32 off) {
+    return reinterpret_cast<const u64*>(reinterpret_cast<const char*>(tab) + off);
 }
 
 // ---------------------------------------------------------------------------
@@ -348,27 +376,38 @@ __device__ __forceinline__ void kth_table_init(uint8_t* tab) {
         for (; k < 8; k++) tab[b * 8 + k] = 0;
     }
 }
-// c_lo = __popc((u32)x), which the caller has from counting x (popcount_lo)
-__device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
+// (a + b) << 3 as one v_add_lshl_u32 (hipcc otherwise distributes the shift
+// over the terms of a, one v_lshlrev_b32 each)
+__device__ __forceinline__ u32 add_lshl3(u32 a, u32 b) {
+    u32 r;
+    asm("v_add_lshl_u32 %0, %1, %2, 3" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// c_lo = __popc((u32)x), which the caller has from counting x (popcount_lo).
+// Returns 8 x the square: the byte offset of the square's entries in the LDS
+// ray table.  Each level keeps k as min(k, k - c) (the unsigned difference
+// wraps when the bit lies below), the byte is one v_bfe_u32 at the last
+// level's offset, and the three level offsets are disjoint bits (32 | 16 | 8):
+// one v_or3 and one v_add_lshl with the table entry give the offset
+// (31 -> 24 VALU per pick with the address arithmetic).
+__device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
     const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 c = c_lo;
-    bool up = k >= c;
+    const bool up = k >= c_lo;
     u32 w = up ? hi : lo;
-    k = up ? k - c : k;
-    u32 pos = up ? 32u : 0u;
-    c = __popc(w & 0xFFFFu);
-    up = k >= c;
-    k = up ? k - c : k;
-    u32 s = up ? 16u : 0u;
-    w >>= s;
-    pos += s;
+    const u32 b32 = up ? 32u : 0u;
+    k = min(k, k - c_lo);
+    u32 c = __popc(w & 0xFFFFu);
+    const u32 s16 = k >= c ? 16u : 0u;
+    k = min(k, k - c);
+    w >>= s16;
     c = __popc(w & 0xFFu);
-    up = k >= c;
-    k = up ? k - c : k;
-    s = up ? 8u : 0u;
-    w >>= s;
-    pos += s;
-    return pos + tab[(w & 0xFFu) * 8u + k];
+    const u32 s8 = k >= c ? 8u : 0u;
+    k = min(k, k - c);
+    const u32 byte = __builtin_amdgcn_ubfe(w, s8, 8);
+    return add_lshl3(b32 | s16 | s8, tab[byte * 8u + k]);
+}
+__device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
+    return kth_bit_off(x, k, c_lo, tab) >> 3;
 }
 
 // index of the k-th set bit (LSB-first, 0-based) of x; requires k < popcount(x).

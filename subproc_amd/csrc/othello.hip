@@ -73,6 +73,11 @@ __device__ __forceinline__ u32 pick_legal(u64 legal, GameRng& rng, const uint8_t
     const u32 c_lo = __popc((u32)legal);
     return kth_bit_tab(legal, rng.pick(c_lo + __popc((u32)(legal >> 32))), c_lo, kth_tab);
 }
+// the same pick as 8 x the square (the byte offset into the LDS ray table)
+__device__ __forceinline__ u32 pick_legal_off(u64 legal, GameRng& rng, const uint8_t* kth_tab) {
+    const u32 c_lo = __popc((u32)legal);
+    return kth_bit_off(legal, rng.pick(c_lo + __popc((u32)(legal >> 32))), c_lo, kth_tab);
+}
 
 // counts() region masks a..h (parameter_progress_position_moves_learn.py:9-16)
 __constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
@@ -110,9 +115,8 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // choice: (score << 6) | square.
 template <int POLICY>
 __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab) {
-    const u64 mv = square_bit(sq, rays);
-    const u64 f = flips_rays(sq, mv, s, rays);
-    const u64 P2 = or3(P, f, mv), O2 = andn(O, f);
+    u64 P2 = P, O2 = O;
+    place(P2, O2, flips_rays(sq, s, rays));
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
     // every child has popcount(P|O) + 1 discs: one weight row per parent
     const int* row = w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
@@ -559,59 +563,65 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
             // (kept separate: this exact loop is the measured config-3 kernel).  A
             // plain divergent loop: a lane leaves it with `break` at its terminal
             // and the loop runs while any lane is left, on the exec mask alone
-            // (no per-iteration ballot).  The side to move is not tracked: P is
-            // side0's discs iff ply is even.  A pass is counted when it is
-            // handed over and uncounted at a terminal, so the common path only
-            // adds 1 to ply.
-            const u32 side0 = side;
+            // (no per-iteration ballot).  The loop body is two plies, side0 to
+            // move and then the other side (a pass also hands the move over), so
+            // P stays side0's discs and O the other side's with no register
+            // swap.  Without a move record the ply counter is not kept either:
+            // every placement adds one disc, so plies = discs placed + passes
+            // handed over (a pass just before the terminal is not an env-step).
+            const bool b0 = side == OTH_BLACK;
+            const u32 discs0 = RECORD ? 0u : (u32)__popcll(P | O);
+            u32 npass = 0;  // passes (RECORD: every ply)
+            // one ply of mover X against Y (X black iff x_black); true at the terminal
+            auto ply_of = [&](u64& X, u64& Y, const bool x_black) -> bool {
+#ifdef OTH_DIAG
+                diag_iters++;
+#endif
+                Position pos;
+                analyse(X, Y, pos);
+                const u64 legal = pos.legal;
+                if (legal == 0) {
+                    // a full board is terminal at once: the other side has no
+                    // empty square either, so the hand-over iteration (a
+                    // second analysis) is skipped; 65% of random games end so
+                    if (passed || (X | Y) == ~0ull) {
+                        // terminal: both sides without a legal move (board.py:57-58);
+                        // a pass handed over just before is not an env-step
+                        if (passed) npass--;
+                        const u32 ply = RECORD ? npass : (u32)__popcll(X | Y) - discs0 + npass;
+                        if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
+                        const u64 bl = x_black ? X : Y, wh = x_black ? Y : X;
+                        const int d = __popcll(bl) - __popcll(wh);
+                        if (a.final_boards)
+                            reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
+                        if (a.diff) a.diff[g] = (int8_t)d;
+                        if (a.plies) a.plies[g] = (uint8_t)ply;
+                        atomicAdd(&hist_s[d + 64], 1ull);
+                        atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
+                        plies_sum += ply;
+                        return true;
+                    }
+                    // the mover must pass ('PS'): hand the move over
+                    if (RECORD && npass < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + npass] = OTH_PASS;
+                    passed = true;
+                    npass++;
+                    return false;
+                }
+                passed = false;
+                const u32 off = pick_legal_off(legal, rng, kth_tab);
+                const u64* col = ray_col(rays, off);
+                const Flips f = flips_col(col[kRayRows * 64], run_sets(pos), col);
+                if (RECORD) {
+                    if (npass < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + npass] = (uint8_t)(off >> 3);
+                    npass++;
+                }
+                place(X, Y, f);
+                return false;
+            };
             if (active) {
                 for (;;) {
-#ifdef OTH_DIAG
-                    diag_iters++;
-#endif
-                    Position pos;
-                    analyse(P, O, pos);
-                    const u64 legal = pos.legal;
-                    if (legal == 0) {
-                        // a full board is terminal at once: the other side has no
-                        // empty square either, so the hand-over iteration (a
-                        // second analysis) is skipped; 65% of random games end so
-                        const bool full = (P | O) == ~0ull;
-                        if (passed || full) {
-                            // terminal: both sides without a legal move (board.py:57-58);
-                            // a pass handed over just before is not an env-step
-                            const bool p_black = (side0 == OTH_BLACK) == ((ply & 1u) == 0u);
-                            if (passed) ply--;
-                            if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
-                            const u64 bl = p_black ? P : O, wh = p_black ? O : P;
-                            const int d = __popcll(bl) - __popcll(wh);
-                            if (a.final_boards)
-                                reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
-                            if (a.diff) a.diff[g] = (int8_t)d;
-                            if (a.plies) a.plies[g] = (uint8_t)ply;
-                            atomicAdd(&hist_s[d + 64], 1ull);
-                            atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
-                            plies_sum += ply;
-                            break;
-                        }
-                        // the mover must pass ('PS'): hand the move over
-                        if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
-                        passed = true;
-                        const u64 t = P;
-                        P = O;
-                        O = t;
-                        ply++;
-                        continue;
-                    }
-                    passed = false;
-                    const u32 sq = pick_legal(legal, rng, kth_tab);
-                    const u64 mv = square_bit(sq, rays);
-                    const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
-                    if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
-                    const u64 np = andn(O, f);
-                    O = or3(P, f, mv);
-                    P = np;
-                    ply++;
+                    if (ply_of(P, O, b0)) break;
+                    if (ply_of(O, P, !b0)) break;
                 }
             }
         } else {
@@ -667,11 +677,11 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     if (choose) sq = c;
                 }
                 if (moving) {
-                    const u64 mv = square_bit(sq, rays);
-                    const u64 f = flips_rays(sq, mv, run_sets(pos), rays);
+                    const Flips f = flips_rays(sq, run_sets(pos), rays);
                     if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
-                    const u64 np = andn(O, f);
-                    O = or3(P, f, mv);
+                    place(P, O, f);
+                    const u64 np = O;
+                    O = P;
                     P = np;
                     side ^= 3u;
                     ply++;

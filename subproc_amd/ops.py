@@ -203,7 +203,10 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     White plays ``weights_white`` (oth_rollout_match).
 
     ``work`` (int64 (1,) device tensor, 0 at the launch) is the launch's batch
-    counter; default: the current stream's :func:`work_word`.
+    counter; default: the current stream's :func:`work_word`.  Under graph
+    capture ``work`` is required: a replay runs on the replaying stream, so
+    every captured launch needs a word of its own, zeroed before the capture
+    (graphs replayed concurrently must not share one).
     """
     if policy not in _POLICIES:
         raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
@@ -223,6 +226,10 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
     if _POLICIES[policy] != POLICY_EVAL and (weights is not None or weights_white is not None):
         raise ValueError("weights apply to policy 'eval' only")
+    capturing = torch.cuda.is_current_stream_capturing()
+    if work is None and capturing:
+        raise RuntimeError("ops.rollout under graph capture needs an explicit work word: an int64 (1,) device "
+                           "tensor zeroed before the capture, one per captured launch")
     w = work_word(d) if work is None else work
     pw = _dev(w, "work", torch.int64, (1,), d)
 
@@ -243,7 +250,13 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
             rc, what = _lib.load().oth_rollout(ps, pst, seed64, game_id0, _POLICIES[policy], n_random, ptr(fb),
                                                ptr(df), ptr(pl), ptr(mv), ph, pw, n, _stream()), "oth_rollout"
         if rc != _lib.OTH_OK:
-            w.zero_()  # a failed launch leaves the counter unknown (include/othello.h)
+            # a failed launch leaves the counter unknown (include/othello.h): the
+            # stream's default word is dropped (the next call makes a fresh zeroed
+            # one); a caller's word is reset eagerly, never as a captured node
+            if work is None:
+                _WORK.pop((d.index, torch.cuda.current_stream().cuda_stream), None)
+            elif not capturing:
+                w.zero_()
         check(rc, what)
     return RolloutResult(fb, df, pl, mv, hist)
 

@@ -64,7 +64,10 @@ def _payload(black_name, white_name, black_wins, white_wins, n_books, diffs_sort
     }
 
 
-def store_batch_stats(books, store=None, win_rule="correct", device="cuda", count_fn=None):
+PARAMS_ORDERS = ("sorted", "set")
+
+
+def store_batch_stats(books, store=None, win_rule="correct", device="cuda", count_fn=None, params_order="sorted"):
     """LearnBasePlus.store_batch_stats(books) (learn_base.py:58-110).
 
     ``books``: [(book_id, records, meta), ...] as replearn.learn_books builds
@@ -73,13 +76,21 @@ def store_batch_stats(books, store=None, win_rule="correct", device="cuda", coun
     payload with ``store.hmset(key, payload)`` when a parameter store is given
     (parameter_store.py:38) and returns ``(key, payload)``.
 
-    ``params_used`` joins the distinct 'hamletparam' values with ' / ' in
-    sorted order (the reference joins a ``set``, whose order is its hash order).
+    ``params_used`` joins the distinct 'hamletparam' values with ' / '.  The
+    reference joins a ``set`` (learn_base.py:95), so its order is the set's
+    iteration order, which CPython randomises per process for strings
+    (PYTHONHASHSEED).  ``params_order="sorted"`` (the default) sorts them, a
+    deterministic order; ``"set"`` joins a set built by the same ``add`` calls in
+    the same order, which reproduces the reference's string exactly in the same
+    interpreter and hash seed (tests/test_stats.py runs it under
+    PYTHONHASHSEED=0 against tests/golden/batch_stats.json).
     ``count_fn(boards (n, 2) uint64) -> (n_black, n_white)`` replaces the
     device count (host tests only); by default the discs are counted by
     ``oth_result`` on ``device``.
     """
     _check_rule(win_rule)
+    if params_order not in PARAMS_ORDERS:
+        raise ValueError(f"params_order must be one of {PARAMS_ORDERS}, got {params_order!r}")
     # pass 1: the terminal boards (learn_base.py:69-71); a book that raises
     # here has no effect but its share of len(books)
     ok, boards = [], []
@@ -125,7 +136,7 @@ def store_batch_stats(books, store=None, win_rule="correct", device="cuda", coun
     if not disc_diff:
         raise ValueError("min() arg is an empty sequence")  # learn_base.py:92: no book was readable
     payload = _payload(black_name, white_name, black_wins, white_wins, len(books), sorted(disc_diff),
-                       " / ".join(sorted(params)))
+                       " / ".join(sorted(params) if params_order == "sorted" else params))
     key = stats_key(min(book_ids), max(book_ids))
     if store is not None:
         store.hmset(key, payload)

@@ -1,7 +1,7 @@
 """Backends for the drop-in Board facade in the tests.
 
 The facade (subproc_amd/board.py) sends every rule question to a device object
-(``board._DEV``) with four calls: legal, result, step, hands.  On the GPU box
+(``board._TLS.dev``, this thread's) with four calls: legal, result, step, hands.  On the GPU box
 that is the HIP library.  For the CPU suite, :class:`CpuAbiDevice` answers the
 same four calls from libothello_cpu.so -- include/othello.h built for the host
 over the oracle (test infrastructure) -- so the facade's own host logic
@@ -64,9 +64,9 @@ BACKENDS = ["cpu_abi", pytest.param("gpu", marks=pytest.mark.gpu)]
 def facade(request):
     """subproc_amd.board with its device calls served by `request.param`."""
     from subproc_amd import board as gboard
-    saved = gboard._DEV
-    gboard._DEV = CpuAbiDevice() if request.param == "cpu_abi" else gboard._Device()
+    saved = getattr(gboard._TLS, "dev", None)
+    gboard._TLS.dev = CpuAbiDevice() if request.param == "cpu_abi" else gboard._Device()
     try:
         yield gboard
     finally:
-        gboard._DEV = saved
+        gboard._TLS.dev = saved

@@ -688,5 +688,159 @@ def main():
     print("fixtures written to", OUT)
 
 
+# ----------------------------------------------------------------------------
+# §8f row 3: LearnBasePlus.store_batch_stats run from the reference itself
+# ----------------------------------------------------------------------------
+def load_reference_learn_base():
+    """learn_base.py exec'd against the shimmed board module and a stub `slack`
+    module (its post_message only records the text: no network).  One in-memory
+    substitution, learn_base.py:87's Python 2 print statement -> print(...);
+    nothing is written to /root/reference and no source is copied."""
+    import types
+    src = open("/root/reference/learn_base.py").read()
+    a = "print 'Exception occured while processing %d th book' % book_id\n"
+    assert src.count(a) == 1, "learn_base.py changed; the shim substitution no longer applies"
+    src = src.replace(a, "print('Exception occured while processing %d th book' % book_id)\n")
+    mod_board = types.ModuleType("board")
+    mod_board.__dict__.update(RB)
+    mod_slack = types.ModuleType("slack")
+    mod_slack.messages = []
+    mod_slack.post_message = mod_slack.messages.append
+    saved = {k: sys.modules.get(k) for k in ("board", "slack")}
+    sys.modules["board"], sys.modules["slack"] = mod_board, mod_slack
+    try:
+        ns = {"__name__": "reference_learn_base"}
+        exec(compile(src, "reference_learn_base.py", "exec"), ns)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return ns, mod_slack
+
+
+def replay_terminal(sb, sw, st, moves):
+    """The terminal record a game's recorder writes (game_recorder.py:107-114):
+    the board after the recorded move codes, driven through board.py's put_s."""
+    b = from_bits(int(sb), int(sw), int(st))
+    for c in moves:
+        if c == 0xFF:
+            break
+        b.put_s(code_to_str(b, int(c)))
+    return {"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn, "end": True}
+
+
+def batch_stats_fixtures():
+    """batch_stats.json: books -> the (key, payload) LearnBasePlus.store_batch_stats
+    (learn_base.py:58-110) hands its parameter store's hmset, run from the
+    reference.  The payload's params_used joins a set: its order is the set's
+    iteration order, which Python 3 randomises per process for strings, so the
+    generator runs under PYTHONHASHSEED=0 and records that."""
+    import fnmatch
+    import subprocess
+    if os.environ.get("PYTHONHASHSEED") != "0":
+        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--only", "batch_stats"],
+                              env=dict(os.environ, PYTHONHASHSEED="0"))
+        return
+    ns, slack = load_reference_learn_base()
+
+    class Store:  # the ParameterStore calls store_batch_stats and __show_stats make
+        def __init__(self):
+            self.calls, self.h = [], {}
+
+        def configure(self, conf):
+            pass
+
+        def hmset(self, key, mapping):
+            self.calls.append((list(key), dict(mapping)))
+            self.h[":".join(key)] = dict(mapping)
+
+        def keys(self, pattern):
+            return [k for k in self.h if fnmatch.fnmatch(k, ":".join(pattern))]
+
+        def hgetall(self, k):
+            return self.h[k]
+
+    class RefLearn(ns["LearnBasePlus"]):
+        def __init__(self):
+            super().__init__()
+            self.store = Store()
+
+        def name(self):
+            return "gpu"
+
+        def _param_store(self):
+            return self.store
+
+    def run(books):
+        lrn = RefLearn()
+        lrn.store_batch_stats([(i, [dict(r) for r in recs] if isinstance(recs, list) else recs,
+                                dict(m) if isinstance(m, dict) else m) for i, recs, m in books])
+        assert len(lrn.store.calls) == 1
+        return lrn.store.calls[0]
+
+    cases = []
+
+    def case(name, books, note=""):
+        key, payload = run(books)
+        cases.append({"name": name, "note": note, "books": [list(b) for b in books], "key": key, "payload": payload})
+
+    def fixture_books(src, meta, id0=None, params=None):
+        z = np.load(os.path.join(OUT, src + ".npz"), allow_pickle=False)
+        g0 = int(z["game_id0"]) if id0 is None else id0
+        books = []
+        for i in range(len(z["final_black"])):
+            term = replay_terminal(z["start_black"][i], z["start_white"][i], z["start_turn"][i], z["moves"][i])
+            m = dict(meta)
+            if params:
+                m["hamletparam"] = params[i % len(params)]
+            books.append((g0 + i, [term, {"book": "", "whosturn": "O", "turn": 0, "end": False}], m))
+            # the replayed terminal board is the fixture's final board
+            b = Board()
+            b.deserialize(term["book"], term["whosturn"], term["turn"])
+            fb, fw = to_bits(b)
+            assert (fb, fw) == (int(z["final_black"][i]), int(z["final_white"][i])), (src, i)
+        return books
+
+    meta = {"proc_a": "Edax", "proc_b": "Hamlet", "hamletparam": "p0"}
+    for src in ("rollout_random", "rollout_greedy", "rollout_random_from_mid", "rollout_match"):
+        case(src, fixture_books(src, meta), "terminal records replayed through board.py from the fixture's moves")
+    case("multi_param", fixture_books("rollout_random_offset", meta, params=["pA", "pB", "pC"]),
+         "three hamletparam values: params_used is ' / '.join(set) in the generator's set order (PYTHONHASHSEED=0)")
+    # line 77: a Black win, then two draws; White's discs are compared with the
+    # running count of Black wins, so both draws count as White wins
+    full, half = (1 << 64) - 1, (1 << 32) - 1
+
+    def rec(bl, wh, turn="O"):
+        return {"book": from_bits(bl, wh, Black).serialize_board(), "whosturn": turn, "turn": 60, "end": True}
+
+    case("line77", [(0, [rec(full ^ 1, 1)], meta), (1, [rec(half, full ^ half)], meta),
+                    (2, [rec(0xFF, 0xFF00)], meta)], "Black win then two draws")
+    # malformed books: learn_base.py:66-88's try (tests/test_stats.py shapes)
+    rng = np.random.default_rng(0)
+    bl = rng.integers(0, 2**63, 12, dtype=np.int64).astype(np.uint64) << np.uint64(1)
+    wh = rng.integers(0, 2**63, 12, dtype=np.int64).astype(np.uint64) & ~bl
+    books = [(100 + i, [rec(int(bl[i]), int(wh[i]))], dict(meta)) for i in range(12)]
+    books[1] = (101, [], dict(meta))                                      # empty book: IndexError at book[0]
+    books[2][1][0]["book"] += "O"                                          # 65 cells: IndexError in deserialize
+    books[3][1][0]["book"] = "XXXXOOOO"                                    # short: over Board()'s opening
+    del books[4][1][0]["whosturn"]                                         # KeyError before counting
+    books[5] = (105, books[5][1], {"proc_a": "C"})                        # counted; names stop at proc_b
+    books[6] = (106, books[6][1], None)                                   # counted; meta unreadable
+    books[7] = (107, books[7][1], {"proc_a": "D", "proc_b": "E", "hamletparam": "p1"})
+    books[8][1][0]["book"] = "".join(rng.choice(list("OX-?o "), 64))      # other characters -> Empty
+    case("malformed", books, "learn_base.py:85-88: a book that raises stops where it raised, "
+                             "and still counts in len(books)")
+    out = {"source": "/root/reference/learn_base.py:58-110 exec'd by gen_golden.py (print shim at :87, "
+                     "stub slack, dict parameter store)",
+           "pythonhashseed": os.environ.get("PYTHONHASHSEED"), "cases": cases}
+    json.dump(out, open(os.path.join(OUT, "batch_stats.json"), "w"))
+    print("batch_stats.json:", len(cases), "cases;", len(slack.messages), "slack messages captured")
+
+
 if __name__ == "__main__":
-    main()
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "batch_stats":
+        batch_stats_fixtures()
+    else:
+        main()

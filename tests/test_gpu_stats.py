@@ -85,3 +85,19 @@ def test_full_size_config3_stats_and_store():
     for rule in stats.WIN_RULES:
         assert stats.rollout_batch_stats(r.final_boards[sub], win_rule=rule) == ref.store_batch_stats(
             books, rule == "reference")
+
+
+def test_store_batch_stats_vs_reference_payload_device_count():
+    """tests/golden/batch_stats.json (learn_base.py:58-110 run from the
+    reference): the books' discs counted by oth_result on the GPU, every field
+    of the key and payload equal (params_used up to the set order, which
+    tests/test_stats.py pins byte for byte under the generator's hash seed)."""
+    from golden_io import load_json
+
+    for case in load_json("batch_stats.json")["cases"]:
+        books = [(i, r, m) for i, r, m in case["books"]]
+        key, payload = stats.store_batch_stats(books, win_rule="reference", device=DEV)
+        want = dict(case["payload"])
+        want["params_used"] = " / ".join(sorted(want["params_used"].split(" / ")))
+        assert key == case["key"], case["name"]
+        assert payload == want, case["name"]

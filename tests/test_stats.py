@@ -88,3 +88,68 @@ def test_store_is_written_and_errors_match():
         stats.store_batch_stats([(1, [], {})], count_fn=count)
     with pytest.raises(ValueError):
         stats.store_batch_stats(books, win_rule="other", count_fn=count)
+
+
+# ---------------------------------------------------------------------------
+# pinned to the reference itself: tests/golden/batch_stats.json holds the
+# (key, payload) learn_base.py:58-110 handed its parameter store's hmset for
+# each batch of books, run from /root/reference by gen_golden.py
+# ---------------------------------------------------------------------------
+def _ref_cases():
+    from golden_io import load_json
+    return load_json("batch_stats.json")
+
+
+def _books(case):
+    return [(i, recs, meta) for i, recs, meta in case["books"]]
+
+
+def _sorted_params(payload):
+    p = dict(payload)
+    p["params_used"] = " / ".join(sorted(p["params_used"].split(" / ")))
+    return p
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in _ref_cases()["cases"]])
+def test_store_batch_stats_vs_reference_payload(name):
+    """Every field of the reference's payload and its key, with win_rule
+    'reference'; params_used up to the set order (sorted on our side)."""
+    case = next(c for c in _ref_cases()["cases"] if c["name"] == name)
+    key, payload = stats.store_batch_stats(_books(case), win_rule="reference", count_fn=count)
+    assert key == case["key"]
+    assert payload == _sorted_params(case["payload"])
+    # the restatement the other tests check against agrees with the reference too
+    assert ref.store_batch_stats(_books(case), reference_rule=True) == (case["key"], _sorted_params(case["payload"]))
+
+
+def test_store_batch_stats_byte_exact_in_the_reference_hash_order():
+    """params_order='set' joins the set as learn_base.py:95 does: in an
+    interpreter with the generator's PYTHONHASHSEED every (key, payload) equals
+    the reference's byte for byte (as JSON), params_used order included."""
+    import json
+    import os
+    import subprocess
+    import sys
+    d = _ref_cases()
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = r'''
+import json, sys
+sys.path[:0] = [%r, %r]
+import numpy as np
+from golden_io import load_json
+from subproc_amd import stats
+def count(b):
+    a = np.ascontiguousarray(b, np.uint64)
+    pc = lambda v: np.unpackbits(v.view(np.uint8).reshape(-1, 8), axis=1).sum(axis=1)
+    return pc(a[:, 0].copy()), pc(a[:, 1].copy())
+out = []
+for c in load_json("batch_stats.json")["cases"]:
+    books = [(i, r, m) for i, r, m in c["books"]]
+    key, payload = stats.store_batch_stats(books, win_rule="reference", count_fn=count, params_order="set")
+    out.append(json.dumps([key, payload]) == json.dumps([c["key"], c["payload"]]))
+print(json.dumps(out))
+''' % (here, os.path.dirname(here))
+    env = dict(os.environ, PYTHONHASHSEED=d["pythonhashseed"])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == [True] * len(d["cases"])

@@ -67,6 +67,10 @@ def valu_entry(kernel, achieved, **extra):
 
 STEP_BYTES = 52  # algorithmic bytes per oth_step: in 16+1+1, out 16+1+8+8+1
 LAUNCH_EVENTS = os.environ.get("BENCH_LAUNCH_EVENTS", "1") == "1"
+PREWARM_SYNC = os.environ.get("BENCH_PREWARM_SYNC") == "1"  # diag: the round-2 pre-warm (a sync per launch)
+# tests only: BENCH_DIST_BACKEND=gloo runs the N>1 line's collectives over gloo on
+# host copies, so two ranks can share one GPU (RCCL needs one GPU per rank)
+DIST_BACKEND = os.environ.get("BENCH_DIST_BACKEND", "nccl")
 ROLLOUT_BYTES_PER_GAME = 18  # final board 16 + diff 1 + plies 1 written; opening generated in-kernel
 
 
@@ -126,13 +130,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    # one rank per GPU; a box with fewer GPUs than ranks (the test that runs
+    # two ranks on one GPU over gloo) puts ranks on GPU local % count
+    ngpu = torch.cuda.device_count()
+    local = local % ngpu if ngpu else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # BENCH_FORCE_DIST=1 runs the RCCL path (barrier, per-step histogram
     # all-reduce, max-over-ranks timing) even at world size 1
     use_dist = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        if DIST_BACKEND == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from subproc_amd import ops
 
@@ -146,7 +157,7 @@ def main():
     def max_over_ranks(x):
         if not use_dist:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if DIST_BACKEND != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -281,6 +292,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
         if k is not None and LAUNCH_EVENTS:
             l1[k].record(st)
         if use_dist and args.allreduce != "end":
+            if DIST_BACKEND == "gloo":
+                raise SystemExit("bench: BENCH_DIST_BACKEND=gloo supports --allreduce end only")
             # config 4: the one collective, ordered after this step's rollout on its stream.
             # Async on RCCL's stream, so it overlaps the next steps (each step owns its
             # histogram row); all are waited for inside the timed region.
@@ -306,13 +319,24 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
             stream.wait_event(e)
 
     # clock pre-warm (untimed, local, no collective): the GPU ramps its clock
-    # over the first ~100 ms of work, longer than a few warmup steps take
+    # over the first ~100 ms of work, longer than a few warmup steps take.  The
+    # launches go round-robin on the bench's streams with no host sync between
+    # them (a sync every 16 bounds the queue), the load the timed steps put on
+    # the chip: with a sync after every launch the first timed region still
+    # ran ~3% slower than the next ones (tools/diag/timeline.py)
     scratch = torch.zeros(HIST_BINS, dtype=torch.int64, device=dev)
     t_w = time.perf_counter()
+    k = 0
+    fork()
     while (time.perf_counter() - t_w) * 1e3 < args.prewarm_ms:
-        fb, df, pl = bufs[0]
-        _lib.check(launch(1 << 52, fb, df, pl, scratch, works[0:1], stream), "rollout")
-        torch.cuda.synchronize()
+        i = k % nstreams
+        fb, df, pl = bufs[i]
+        _lib.check(launch(1 << 52, fb, df, pl, scratch, works[i:i + 1], streams[i]), "rollout")
+        k += 1
+        if PREWARM_SYNC or k % 16 == 0:
+            torch.cuda.synchronize()
+    join()
+    torch.cuda.synchronize()
     fork()
     for s in range(args.warmup):
         one_step(s)
@@ -320,15 +344,20 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     drain()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
     ev0.record(stream)
-    fork()
+    fork()  # host-side set-up of the side streams' start, before the clock starts
+    t0 = time.perf_counter()
     for k, s in enumerate(range(args.warmup, args.warmup + args.steps)):
         one_step(s, k)
     join()
     if use_dist and args.allreduce == "end":
         total = hists[args.warmup:].sum(0)
-        dist.all_reduce(total, op=dist.ReduceOp.SUM)
+        if DIST_BACKEND == "gloo":  # tests only: gloo reduces host memory
+            host = total.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            total.copy_(host)
+        else:
+            dist.all_reduce(total, op=dist.ReduceOp.SUM)
         hists[args.warmup].copy_(total)
         hists[args.warmup + 1:].zero_()
     ev1.record(stream)
@@ -359,7 +388,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
                        "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
                        "streams": nstreams, "env_steps_per_game": env_steps / games, "world_size": world,
                        "game_ids": _game_id_ranges(n, world, args.warmup, args.steps),
-                       "games_counted": counted})
+                       "games_counted": counted, "env_steps": env_steps,
+                       "black_white_draw": [int(v) for v in timed[129:132]]})
     # roofline: algorithmic bytes of one launch / that launch's duration (events on its stream)
     achieved = n * ROLLOUT_BYTES_PER_GAME / (launch_ms * 1e-3) / 1e9
     kname = "rollout_kernel<%d, false>" % pid
@@ -498,9 +528,11 @@ def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):
 
 
 def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
-    """§8f row 1: the book emitter over 262,144 games -- oth_replay (every
-    recorded position, turn and is_game_over) and oth_book_text of all
-    262,144 x 129 rows; HIP events, after 3 untimed launches each."""
+    """§8f row 1: the book emitter over 262,144 games -- the packed-rows replay
+    (oth_replay_rows: each game's plies + 1 recorded positions, turn and
+    is_game_over) and oth_book_text of exactly those rows, as GameBooks runs
+    them; the strided replay (oth_replay, all 129 rows per game) beside it.
+    HIP events, after 3 untimed launches each."""
     r = ops.rollout(games, args.seed, 1 << 40, "random", record_moves=True, device=dev)
     out = {}
 
@@ -516,17 +548,26 @@ def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps * 1e3
 
-    us = timed(lambda: ops.replay(r.moves, r.plies))
-    rows = games * 129
-    # algorithmic bytes: 128-B move record + plies read; 129 rows x (16 + 1 + 1) written
-    rb = games * (128 + 1 + 129 * 18)
-    out["replay"] = {"games": games, "us": us, "achieved_gbs": rb / us / 1e3, "frac_hbm": rb / us / 1e3 / HBM_PEAK_GBS}
-    pos = ops.replay(r.moves, r.plies)
-    b, t = pos.boards.reshape(-1, 2), pos.turn.reshape(-1)
-    us = timed(lambda: ops.book_text(b, t))
+    from subproc_amd import _lib
+    lib = _lib.load()
+    row_off, rows = ops.row_offsets(r.plies)
+    pk = ops.replay_rows(r.moves, r.plies)
+    st = torch.cuda.current_stream().cuda_stream
+    args_rows = (None, None, r.moves.data_ptr(), r.plies.data_ptr(), row_off.data_ptr(), pk.boards.data_ptr(),
+                 pk.turn.data_ptr(), pk.end.data_ptr(), games, st)
+    us = timed(lambda: _lib.check(lib.oth_replay_rows(*args_rows), "oth_replay_rows"))
+    # algorithmic bytes: 128-B move record + plies + row offset read; 18 B per recorded row written
+    rb = games * (128 + 1 + 8) + rows * 18
+    out["replay_rows"] = {"games": games, "rows": rows, "us": us, "achieved_gbs": rb / us / 1e3,
+                          "frac_hbm": rb / us / 1e3 / HBM_PEAK_GBS, "algorithmic_bytes": rb}
+    us = timed(lambda: ops.book_text(pk.boards, pk.turn))
     tb = rows * (16 + 1 + 67)
     out["book_text"] = {"lines": rows, "us": us, "achieved_gbs": tb / us / 1e3, "frac_hbm": tb / us / 1e3 / HBM_PEAK_GBS}
-    out["metric"] = "book emitter (replay + serialize_str text) per 262,144 games"
+    us = timed(lambda: ops.replay(r.moves, r.plies))
+    sb = games * (128 + 1 + 129 * 18)  # the strided table: all 129 rows per game written
+    out["replay_strided"] = {"games": games, "us": us, "achieved_gbs": sb / us / 1e3,
+                             "useful_gbs": rb / us / 1e3, "frac_hbm": sb / us / 1e3 / HBM_PEAK_GBS}
+    out["metric"] = "book emitter (packed replay + serialize_str text) per 262,144 games"
     return out
 
 

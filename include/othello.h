@@ -164,6 +164,28 @@ int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t
 
 /* ---- SURVEY.md §8f "next" rows ------------------------------------------ */
 
+/* GameRunner's match schedule (game_runner.py:104-201 as subproc.do_match,
+ * subproc.py:15-39, runs it) for n games between player A and player B, both
+ * playing `policy`: OTH_POLICY_GREEDY, or OTH_POLICY_EVAL with the eval
+ * tables weights_a / weights_b (HOST pointers, OTH_EVAL_WEIGHTS int8 each;
+ * unused by greedy).  Per game, on its counter RNG stream:
+ *  - colours: with swap_colours != 0 the first draw c = pick(2), and A plays
+ *    White iff c == 1 (do_match's randrange(2), proc_randomize_black_white);
+ *    otherwise A plays Black (proc_a is the black engine, 28-35);
+ *  - random moves: each player starts with min(n_rand, 10) random moves to
+ *    place (n_rand_a / n_rand_b = proc_n_rand_hands_for_a / _b; GameRunner
+ *    caps the budget at N_RAND_HAND_UNTIL, 115-119).  On each of its turns --
+ *    a placement or a pass -- a player with budget r > 0 draws c = pick(r);
+ *    c == 0 and at least one legal move: it plays the legal move of index
+ *    pick(#legal) in puttables order and r -= 1 (go_for, 133-150); otherwise
+ *    it plays its policy's move, or passes.
+ * a_black (n bytes, may be NULL) receives 1 where A played Black.  Everything
+ * else as oth_rollout_match (diff, hist and final boards are by colour). */
+int oth_rollout_runner(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                       const int8_t* weights_a, const int8_t* weights_b, int n_rand_a, int n_rand_b, int swap_colours,
+                       uint8_t* a_black, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
+                       int64_t* hist, uint64_t* work, int64_t n, void* stream);
+
 /* Book emitter, step 1: replay recorded move codes (a rollout's `moves`
  * record, or any put_s code list) into every recorded position, as
  * GameRunner records them (game_runner.py:169-184: after Board() and after each
@@ -176,6 +198,18 @@ int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t
  * pos_end. */
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
                uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream);
+
+/* oth_replay into packed rows: game i's position p (0 <= p <= plies[i], plies
+ * capped at OTH_MOVES_STRIDE) goes to row row_off[i] + p of pos_boards,
+ * pos_turn and pos_end, and only those rows are written -- the useful bytes,
+ * about half of the strided table for random games.  row_off (device, n int64)
+ * must be the exclusive prefix sum of min(plies[i], OTH_MOVES_STRIDE) + 1, so
+ * the rows of all games are one contiguous range of row_off[n-1] +
+ * min(plies[n-1], OTH_MOVES_STRIDE) + 1 rows (oth_book_text serialises them in
+ * one call); other offsets are the caller's risk (rows may overlap). */
+int oth_replay_rows(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+                    const int64_t* row_off, uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n,
+                    void* stream);
 
 /* Book emitter, step 2: serialize_str() (board.py:214-243: 64 chars O/X/-,
  * ' ', side O/X/-) + '\n' for n consecutive positions, concatenated into
@@ -213,6 +247,10 @@ int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights,
  * from bit 35 down to bit 0.  Integer order == tuple order. */
 int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
                    int64_t* keys, double* values, int64_t n, void* stream);
+/* oth_td_updates over an oth_replay_rows table: game g's position p is row
+ * row_off[g] + p (device, n int64). */
+int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
+                        const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream);
 
 /* TD state map, step 2: segment s (updates seg_off[s] .. seg_off[s+1]-1 of one
  * key, in stream order) starts from init[s] and applies, in order,

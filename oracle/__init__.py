@@ -62,12 +62,14 @@ def lib():
         L.oracle_replay.argtypes = [P, P, P, P, P, P, P, I64]
         L.oracle_hands.argtypes = [P, P, P, P, P, P, P, I64]
         L.oracle_rollout_ids.argtypes = [P, I64, U64, I, I, P, P, P, P, P]
+        L.oracle_rollout_runner.argtypes = [P, P, U64, U64, I, P, P, I, I, I, P, P, P, P, P, P, I64, I]
         L.oracle_game_key.argtypes = [U64, U64]
         L.oracle_game_key.restype = U64
         L.oracle_rng_draws.argtypes = [U64, ctypes.c_uint32]
         L.oracle_rng_draws.restype = ctypes.c_uint32
         for f in ("oracle_reset", "oracle_legal", "oracle_step", "oracle_result", "oracle_rollout",
-                  "oracle_sample_midgame", "oracle_features", "oracle_eval", "oracle_replay", "oracle_hands", "oracle_rollout_ids"):
+                  "oracle_sample_midgame", "oracle_features", "oracle_eval", "oracle_replay", "oracle_hands", "oracle_rollout_ids",
+                  "oracle_rollout_runner"):
             getattr(L, f).restype = I
         _lib = L
     return _lib
@@ -147,6 +149,28 @@ def rollout(n, seed, game_id0=0, policy=0, n_random=10, start=None, start_turn=N
     lib().oracle_rollout(_p(start), _p(st), seed, game_id0, policy, n_random, _p(fb), _p(d), _p(pl), _p(mv), _p(h),
                          n, n_threads, _p(w), _p(ww))
     return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h)
+
+
+def rollout_runner(n, seed, game_id0=0, policy=2, weights_a=None, weights_b=None, n_rand_a=0, n_rand_b=0, swap=False,
+                   start=None, start_turn=None, record_moves=False, n_threads=0):
+    """GameRunner matches (include/othello.h oth_rollout_runner): player A vs
+    player B, both greedy (1) or eval (2) with their own tables, GameRunner's
+    random-move budgets and do_match's colour swap.  dict(..., a_black)."""
+    wa = None if weights_a is None else _weights(weights_a)
+    wb = None if weights_b is None else _weights(weights_b)
+    start = None if start is None else _boards(start)
+    st = None if start_turn is None else np.ascontiguousarray(start_turn, np.uint8)
+    fb = np.empty((n, 2), np.uint64)
+    d = np.empty(n, np.int8)
+    pl = np.empty(n, np.uint8)
+    ab = np.empty(n, np.uint8)
+    mv = np.empty((n, MOVES_STRIDE), np.uint8) if record_moves else None
+    h = np.zeros(HIST_BINS, np.int64)
+    rc = lib().oracle_rollout_runner(_p(start), _p(st), seed, game_id0, policy, _p(wa), _p(wb), n_rand_a, n_rand_b,
+                                     int(bool(swap)), _p(ab), _p(fb), _p(d), _p(pl), _p(mv), _p(h), n, n_threads)
+    if rc != 0:
+        raise ValueError("oracle_rollout_runner: invalid arguments")
+    return dict(final_boards=fb, diff=d, plies=pl, moves=mv, hist=h, a_black=ab)
 
 
 def rollout_ids(ids, seed, policy=0, n_random=10, weights=None, weights_white=None):

@@ -29,6 +29,10 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
                    int64_t* hist, int64_t n, int n_threads, const int8_t* weights, const int8_t* weights_white);
 int oracle_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
                           uint8_t* move, int64_t n);
+int oracle_rollout_runner(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                          int policy, const int8_t* weights_a, const int8_t* weights_b, int n_rand_a, int n_rand_b,
+                          int swap, uint8_t* a_black, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                          uint8_t* moves, int64_t* hist, int64_t n, int n_threads);
 int oracle_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n);
 int oracle_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights, int32_t* out, int64_t n);
 int oracle_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
@@ -112,6 +116,19 @@ int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t
                           moves, hist, n, 0, weights_black, weights_white);
 }
 
+int oth_rollout_runner(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                       const int8_t* weights_a, const int8_t* weights_b, int n_rand_a, int n_rand_b, int swap_colours,
+                       uint8_t* a_black, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
+                       int64_t* hist, uint64_t* work, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || !work || (policy != OTH_POLICY_GREEDY && policy != OTH_POLICY_EVAL) ||
+        (policy == OTH_POLICY_EVAL && (!weights_a || !weights_b)) || n_rand_a < 0 || n_rand_b < 0)
+        return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    return oracle_rollout_runner(start, start_turn, seed, game_id0, policy, weights_a, weights_b, n_rand_a, n_rand_b,
+                                 swap_colours, a_black, final_boards, diff, plies, moves, hist, n, 0);
+}
+
 int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
                        uint8_t* move, int64_t n, void* stream) {
     (void)stream;
@@ -124,6 +141,30 @@ int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* 
     (void)stream;
     if (n < 0 || (n > 0 && (!moves || !plies || !pos_boards))) return OTH_EINVAL;
     return oracle_replay(start, start_turn, moves, plies, pos_boards, pos_turn, pos_end, n);
+}
+
+/* the packed-rows layout: the oracle's strided replay of one game at a time,
+ * its rows 0..plies copied to row_off[i] */
+int oth_replay_rows(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+                    const int64_t* row_off, uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n,
+                    void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!moves || !plies || !row_off || !pos_boards))) return OTH_EINVAL;
+    uint64_t b[2 * OTH_POS_STRIDE];
+    uint8_t t[OTH_POS_STRIDE], e[OTH_POS_STRIDE];
+    for (int64_t i = 0; i < n; i++) {
+        int rc = oracle_replay(start ? start + 2 * i : NULL, start_turn ? start_turn + i : NULL,
+                               moves + i * OTH_MOVES_STRIDE, plies + i, b, t, e, 1);
+        if (rc != OTH_OK) return rc;
+        const int np = plies[i] < OTH_MOVES_STRIDE ? plies[i] : OTH_MOVES_STRIDE;
+        for (int p = 0; p <= np; p++) {
+            pos_boards[2 * (row_off[i] + p)] = b[2 * p];
+            pos_boards[2 * (row_off[i] + p) + 1] = b[2 * p + 1];
+            if (pos_turn) pos_turn[row_off[i] + p] = t[p];
+            if (pos_end) pos_end[row_off[i] + p] = e[p];
+        }
+    }
+    return OTH_OK;
 }
 
 /* serialize_str (board.py:214-243) + '\n': 64 chars row-major, 'O' black,
@@ -156,12 +197,10 @@ static int64_t td_key(const uint8_t f[10]) {
     return k;
 }
 
-int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
-                   int64_t* keys, double* values, int64_t n, void* stream) {
-    (void)stream;
-    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
+static int td_updates_any(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
+                          const int64_t* base, const double* lam_pow, int64_t* keys, double* values, int64_t n) {
     for (int64_t g = 0; g < n; g++) {
-        const uint64_t* row = pos_boards + g * OTH_POS_STRIDE * 2;
+        const uint64_t* row = pos_boards + (row_off ? row_off[g] : g * OTH_POS_STRIDE) * 2;
         const int np = plies[g] < OTH_MOVES_STRIDE ? plies[g] : OTH_MOVES_STRIDE;
         int8_t d;
         oracle_result(row + 2 * np, NULL, NULL, &d, NULL, 1);
@@ -178,6 +217,21 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
         }
     }
     return OTH_OK;
+}
+
+int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
+                   int64_t* keys, double* values, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
+    return td_updates_any(pos_boards, NULL, plies, base, lam_pow, keys, values, n);
+}
+
+int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
+                        const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!pos_boards || !row_off || !plies || !base || !lam_pow || !keys || !values)))
+        return OTH_EINVAL;
+    return td_updates_any(pos_boards, row_off, plies, base, lam_pow, keys, values, n);
 }
 
 int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,

@@ -283,18 +283,48 @@ static int eval_of(const Board* s, int t, const int8_t* w) {
     return v;
 }
 
+/* GameRunner's match schedule (game_runner.py:104-152, subproc.py:15-39;
+ * include/othello.h oth_rollout_runner): NULL = the plain rollouts' rule (the
+ * first n_random plies random for both sides). */
+typedef struct {
+    int n_rand_a, n_rand_b; /* proc_n_rand_hands_for_a / _b */
+    int swap;               /* proc_randomize_black_white */
+    const int8_t *w_a, *w_b;
+} Runner;
+
 /* One game to terminal from s, game_runner.py:165-201 loop with the build's
- * policies: a side with no move passes ('PS'). */
+ * policies: a side with no move passes ('PS').  With a
+ * runner schedule: the colour draw first (subproc.py:28-32), then on each turn
+ * of a player with random budget left a coin pick(budget); 0 with a legal move
+ * plays puttables[pick(#legal)] and spends one (go_for, game_runner.py:133-150).
+ * *a_black (runner only) = 1 where player A played Black. */
 static int play_game(Board* s, uint64_t key, int policy, int n_random, const int8_t* w, const int8_t* w_white,
-                     uint8_t* moves) {
+                     uint8_t* moves, const Runner* run, uint8_t* a_black) {
     int ply = 0;
     GameRng rng = rng_init(key);
+    int rem[3] = {0, 0, 0}; /* random budget left, by colour (Black = 1, White = 2) */
+    if (run) {
+        int ab = 1;
+        if (run->swap && rng_pick(&rng, 2) == 1) ab = 0; /* do_match swapped proc_a and proc_b */
+        int ra = run->n_rand_a < 10 ? run->n_rand_a : 10, rb = run->n_rand_b < 10 ? run->n_rand_b : 10;
+        rem[Black] = ab ? ra : rb;
+        rem[White] = ab ? rb : ra;
+        w = ab ? run->w_a : run->w_b;       /* Black's table */
+        w_white = ab ? run->w_b : run->w_a; /* White's table */
+        if (a_black) *a_black = (uint8_t)ab;
+    }
     while (!is_game_over(s)) {
         uint64_t legal = puttables(s, s->turn);
         int code;
+        int coin_random = 0;
+        if (run && (s->turn == Black || s->turn == White) && rem[s->turn] > 0 &&
+            rng_pick(&rng, rem[s->turn]) == 0 && legal) {
+            coin_random = 1;
+            rem[s->turn]--;
+        }
         if (!legal) {
             code = PASS_CODE;
-        } else if (policy == 0 || ply < n_random) {
+        } else if (coin_random || (!run && (policy == 0 || ply < n_random))) {
             code = kth_square(legal, rng_pick(&rng, popcount64(legal)));
         } else if (policy == 1) { /* greedy: minimise the opponent's mobility */
             int best = -1, bestv = 1 << 30;
@@ -327,9 +357,35 @@ static int play_game(Board* s, uint64_t key, int policy, int n_random, const int
 
 /* policy 0 random, 1 greedy, 2 eval (weights: int8[36], used by policy 2 only;
  * weights_white NULL = White uses `weights` too, else White's table: a match) */
+static int rollout_any(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                       int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                       uint8_t* moves, int64_t* hist, int64_t n, int n_threads, const int8_t* weights,
+                       const int8_t* weights_white, const Runner* run, uint8_t* a_black);
+
 int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
                    int64_t* hist, int64_t n, int n_threads, const int8_t* weights, const int8_t* weights_white) {
+    return rollout_any(start, start_turn, seed, game_id0, policy, n_random, final_boards, diff, plies, moves, hist,
+                       n, n_threads, weights, weights_white, 0, 0);
+}
+
+/* GameRunner matches (oth_rollout_runner): policy 1 greedy or 2 eval for both
+ * players, A's and B's eval tables, random budgets and colour swap */
+int oracle_rollout_runner(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                          int policy, const int8_t* weights_a, const int8_t* weights_b, int n_rand_a, int n_rand_b,
+                          int swap, uint8_t* a_black, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                          uint8_t* moves, int64_t* hist, int64_t n, int n_threads) {
+    if ((policy != 1 && policy != 2) || (policy == 2 && (!weights_a || !weights_b)) || n_rand_a < 0 || n_rand_b < 0)
+        return -1;
+    Runner run = {n_rand_a, n_rand_b, swap != 0, weights_a, weights_b};
+    return rollout_any(start, start_turn, seed, game_id0, policy, 0, final_boards, diff, plies, moves, hist, n,
+                       n_threads, weights_a, weights_b, &run, a_black);
+}
+
+static int rollout_any(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0,
+                       int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
+                       uint8_t* moves, int64_t* hist, int64_t n, int n_threads, const int8_t* weights,
+                       const int8_t* weights_white, const Runner* run, uint8_t* a_black) {
     if (policy == 2 && !weights) return -1;
     if (!weights_white) weights_white = weights;
     uint64_t S = seed_state(seed);
@@ -352,7 +408,7 @@ int oracle_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t se
             else board_init(&s);
             if (moves) memset(moves + i * MOVES_STRIDE, 255, MOVES_STRIDE);
             int p = play_game(&s, game_key(S, game_id0 + (uint64_t)i), policy, n_random, weights, weights_white,
-                              moves ? moves + i * MOVES_STRIDE : 0);
+                              moves ? moves + i * MOVES_STRIDE : 0, run, a_black ? a_black + i : 0);
             int d = n_of(&s, Black) - n_of(&s, White);
             uint64_t bl, wh;
             board_to_bits(&s, &bl, &wh);
@@ -386,7 +442,7 @@ int oracle_rollout_ids(const uint64_t* ids, int64_t n, uint64_t seed, int policy
     for (int64_t j = 0; j < n; j++) {
         Board s;
         board_init(&s);
-        int p = play_game(&s, game_key(S, ids[j]), policy, n_random, weights, weights_white, 0);
+        int p = play_game(&s, game_key(S, ids[j]), policy, n_random, weights, weights_white, 0, 0, 0);
         board_to_bits(&s, &final_boards[2 * j], &final_boards[2 * j + 1]);
         diff[j] = (int8_t)(n_of(&s, Black) - n_of(&s, White));
         plies[j] = (uint8_t)p;

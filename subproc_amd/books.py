@@ -11,7 +11,7 @@ learners consume GPU games unchanged.
   game_recorder.py:107-114, 197-205): {'book': serialize_board(),
   'whosturn': serialize_turn(), 'turn': nturn, 'end': is_game_over()}.
 
-The positions come from the HIP replay kernel (``ops.replay``) and the text from
+The positions come from the HIP replay kernel (``ops.replay_rows``) and the text from
 the HIP serializer (``ops.book_text``); only the file assembly (headers,
 slicing per game) is host work.  Redis/DynamoDB I/O itself stays out of scope.
 """
@@ -20,20 +20,24 @@ import os
 import torch
 
 from . import ops
-from ._lib import BOOK_LINE, POS_STRIDE
+from ._lib import BOOK_LINE, MOVES_STRIDE
 
 
 class GameBooks:
-    """Books of n games played on the GPU (a rollout with ``record_moves=True``)."""
+    """Books of n games played on the GPU (a rollout with ``record_moves=True``).
+
+    The recorded positions are replayed into packed rows (``ops.replay_rows``:
+    game g's boards are rows ``row_off[g] .. row_off[g] + plies[g]``) and the
+    text is serialised over exactly those rows, so neither kernel touches the
+    unused tail of a 129-row stride."""
 
     def __init__(self, moves, plies, start=None, start_turn=None):
         self.plies = plies
         self.n = moves.shape[0]
-        self.pos = ops.replay(moves, plies, start, start_turn)
-        flat_b = self.pos.boards.view(-1, 2)
-        flat_t = self.pos.turn.view(-1)
-        self._text = ops.book_text(flat_b, flat_t)  # n * 129 lines, 67 bytes each
+        self.pos = ops.replay_rows(moves, plies, start, start_turn)
+        self._text = ops.book_text(self.pos.boards, self.pos.turn)  # one 67-byte line per recorded board
         self._plies_host = None
+        self._off_host = None
 
     @classmethod
     def from_rollout(cls, r, start=None, start_turn=None):
@@ -43,30 +47,36 @@ class GameBooks:
 
     def _plies(self):
         if self._plies_host is None:
-            self._plies_host = self.plies.cpu().tolist()
+            self._plies_host = [min(p, MOVES_STRIDE) for p in self.plies.cpu().tolist()]
         return self._plies_host
+
+    def _rows(self, g):
+        """(first row, row count) of game g in the packed tables."""
+        if self._off_host is None:
+            self._off_host = self.pos.row_off.cpu().tolist()
+        return self._off_host[g], self._plies()[g] + 1
+
+    def _body(self, g):
+        r0, k = self._rows(g)
+        return self._text[r0 * BOOK_LINE:(r0 + k) * BOOK_LINE].cpu().numpy().tobytes()
 
     def lines(self, g):
         """serialize_str() of every recorded board of game g (board.py:214-221)."""
-        p = self._plies()[g]
-        raw = self._text[g * POS_STRIDE * BOOK_LINE:(g * POS_STRIDE + p + 1) * BOOK_LINE].cpu().numpy().tobytes()
-        return raw.decode("ascii").splitlines()
+        return self._body(g).decode("ascii").splitlines()
 
     def flat_file_bytes(self, g, black_name="gpu_black", white_name="gpu_white"):
         """Exactly the bytes FlatFileRecorder.store() writes (game_recorder.py:67-76)."""
-        p = self._plies()[g]
-        body = self._text[g * POS_STRIDE * BOOK_LINE:(g * POS_STRIDE + p + 1) * BOOK_LINE].cpu().numpy().tobytes()
-        return ("%% Black: %s\n%% White: %s\n" % (black_name, white_name)).encode("ascii") + body
+        return ("%% Black: %s\n%% White: %s\n" % (black_name, white_name)).encode("ascii") + self._body(g)
 
     def write_flat_files(self, out_dir, title="gpu", black_name="gpu_black", white_name="gpu_white", games=None):
         """One FlatFileRecorder-format file per game: <out_dir>/<title>_<g>."""
         os.makedirs(out_dir, exist_ok=True)
         games = range(self.n) if games is None else games
         text = self._text.cpu().numpy()
-        pl = self._plies()
         paths = []
         for g in games:
-            body = text[g * POS_STRIDE * BOOK_LINE:(g * POS_STRIDE + pl[g] + 1) * BOOK_LINE].tobytes()
+            r0, k = self._rows(g)
+            body = text[r0 * BOOK_LINE:(r0 + k) * BOOK_LINE].tobytes()
             path = os.path.join(out_dir, "%s_%d" % (title, g))
             with open(path, "wb") as f:
                 f.write(("%% Black: %s\n%% White: %s\n" % (black_name, white_name)).encode("ascii"))
@@ -76,16 +86,20 @@ class GameBooks:
 
     def records(self, g):
         """RedisRecorder.add() dicts of game g, in recording order."""
-        p = self._plies()[g]
-        end = self.pos.end[g, :p + 1].cpu().tolist()
-        out = []
-        for k, line in enumerate(self.lines(g)):
-            out.append({"book": line[:64], "whosturn": line[65], "turn": k, "end": bool(end[k])})
-        return out
+        r0, k = self._rows(g)
+        end = self.pos.end[r0:r0 + k].cpu().tolist()
+        return [{"book": line[:64], "whosturn": line[65], "turn": p, "end": bool(end[p])}
+                for p, line in enumerate(self.lines(g))]
 
     def features(self, side):
         """counts() features (ops.features) of every recorded position for side
-        1 ('O') or 2 ('X'): (n, 129, 10) uint8; rows past plies are undefined."""
-        flat = self.pos.boards.view(-1, 2)
+        1 ('O') or 2 ('X'): (R, 10) uint8 in the packed row order (game g's
+        positions are rows ``game_rows(g)``)."""
+        flat = self.pos.boards
         sd = torch.full((flat.shape[0],), side, dtype=torch.uint8, device=flat.device)
-        return ops.features(flat, sd).view(self.n, POS_STRIDE, -1)
+        return ops.features(flat, sd)
+
+    def game_rows(self, g):
+        """The slice of game g's rows in pos / features / the text lines."""
+        r0, k = self._rows(g)
+        return slice(r0, r0 + k)

@@ -39,8 +39,8 @@ __device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
     return ((u64)hi << 32) | lo;
 }
 // The three-input logic of these kernels goes through v_bitop3_b32 by hand:
-// measured on the box (tools/diag/valu_rate4.cpp, 8 waves/SIMD) it issues in
-// 2.4-3.4 cycles per wave-instruction where v_bfi_b32 and v_or3_b32 take 4.2,
+// measured on the box (tools/diag/valu_rate5.cpp, 8 waves/SIMD) it issues in
+// 2.4-2.5 cycles per wave-instruction where v_bfi_b32 and v_or3_b32 take 4.2,
 // and hipcc emits bfi / or3 / bfi-with-0 for these forms on its own.
 // bfi(m, a, b) = (m & a) | (~m & b).  Every Kogge-Stone step "gen |= pro &
 // shifted" is written as bfi(pro, shifted, gen): the propagator never
@@ -52,7 +52,7 @@ __device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return bitop3<0xFE>(a,
 // 64-bit shifts as single v_lshlrev_b64 / v_lshrrev_b64 (inline asm): with
 // the 3-input logic taken apart into 32-bit halves, hipcc's combiner would
 // otherwise split each shift into v_lshlrev_b32 + v_alignbit_b32, two
-// instructions where one 64-bit shift issues as fast (valu_rate4.cpp).
+// instructions where one 64-bit shift issues as fast (valu_rate5.cpp).
 template <int S, bool L>
 __device__ __forceinline__ u64 sh(u64 x) {
     static_assert(S > 0 && S < 64, "shift amount");

@@ -176,11 +176,12 @@ __device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, RunSet
     O = r[1];
     s = *reinterpret_cast<const RunSets*>(r + 2);
 }
-// w_s: the two eval tables (Black's, then White's, kEvalTable ints each)
+// w_s: the two eval tables (kEvalTable ints each); tbl (0 / 1) is the mover's
+// (Black's / White's, or in a GameRunner match player A's / B's)
 template <int POLICY>
-__device__ u32 coop_choose(bool need, u64 P, u64 O, u32 side, const Position& pos, CoopWave& cw, const u64* rays,
+__device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, u32 lane, u32 cap) {
-    const u32 white = side == OTH_WHITE ? 64u : 0u;
+    const u32 white = tbl ? 64u : 0u;  // (the list entry's table bit)
     u32 cnt = 0;
     if (need) {
         u64* r = cw.rec[lane];
@@ -489,14 +490,19 @@ struct RolloutArgs {
     unsigned long long* work;  // the caller's work word (0 at start, left at 0)
     u64 last_ticket;           // 64 * (batches + waves - 1): the launch's last dequeue
     u32 coop_cap;              // 1-ply policies: overflow list entries used (kCoopCap; tests lower it)
-    EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table
+    EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table (runner: A's, B's)
+    // GameRunner schedule (RUNNER kernels, oth_rollout_runner): random budgets
+    // of players A and B (already capped at 10), the colour draw, A's colours
+    u32 n_rand_a, n_rand_b;
+    int swap;
+    uint8_t* a_black;
 };
 
 #ifdef OTH_DIAG
 __device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
 #endif
 
-template <int POLICY, bool RECORD>
+template <int POLICY, bool RECORD, bool RUNNER = false>
 __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
     const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
@@ -625,6 +631,16 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
             }
         } else {
+            // GameRunner schedule (RUNNER): the colour draw, then the random
+            // budgets left by colour; tbl_black = the eval table Black plays
+            u32 rem_b = 0, rem_w = 0, tbl_black = 0;
+            if (RUNNER && active) {
+                const bool ab = !(a.swap && rng.pick(2) == 1u);  // do_match's swap (subproc.py:28-32)
+                rem_b = ab ? a.n_rand_a : a.n_rand_b;
+                rem_w = ab ? a.n_rand_b : a.n_rand_a;
+                tbl_black = ab ? 0u : 1u;
+                if (a.a_black) a.a_black[g] = (uint8_t)ab;
+            }
             while (__ballot(active)) {
 #ifdef OTH_DIAG
                 diag_iters++;
@@ -663,16 +679,31 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                             if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
                             ply++;
                             passed = false;
+                            if (RUNNER) {  // the passer's turn drew its coin (go_for, game_runner.py:134-135)
+                                const u32 rx = side == OTH_BLACK ? rem_w : rem_b;
+                                if (rx) (void)rng.pick(rx);
+                            }
                         }
                         moving = true;
-                        if ((int)ply >= a.n_random)
+                        if (RUNNER) {
+                            const u32 r = side == OTH_BLACK ? rem_b : rem_w;
+                            if (r && rng.pick(r) == 0u) {  // go_for's coin: a random legal move (136-146)
+                                sq = pick_legal(legal, rng, kth_tab);
+                                if (side == OTH_BLACK) rem_b--;
+                                else rem_w--;
+                            } else {
+                                choose = true;
+                            }
+                        } else if ((int)ply >= a.n_random) {
                             choose = true;  // decided below, by the whole wave
-                        else
+                        } else {
                             sq = pick_legal(legal, rng, kth_tab);
+                        }
                     }
                 }
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
-                    const u32 c = coop_choose<POLICY>(choose, P, O, side, pos, coop[threadIdx.x >> 6], rays, w_s,
+                    const u32 tbl = side == OTH_BLACK ? tbl_black : tbl_black ^ 1u;
+                    const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, coop[threadIdx.x >> 6], rays, w_s,
                                                       (u32)lane, a.coop_cap);
                     if (choose) sq = c;
                 }
@@ -818,14 +849,29 @@ __device__ __forceinline__ void unstage_byte(u32 c, const uint8_t* start_turn, i
 // contiguous bytes instead of 64 scattered 16-B rows.
 constexpr int kReplayBursts = (OTH_POS_STRIDE + 7 + kReplayBurst - 1) / kReplayBurst;  // 17 for every alignment
 constexpr int kXHalf = kReplayBurst / 2;  // rows per exchange
+// the packed layout's stage: the block's bytes start at a 16-B chunk offset of
+// up to 15, and its turn / end ranges are chunked from there
+constexpr int kReplayStagePacked = kReplayStage + 16;
 
+// Two output layouts (include/othello.h):
+//  * strided (PACKED = false): game i's position p at row i*OTH_POS_STRIDE + p,
+//    every row of the stride written (rows past plies as 0);
+//  * packed (PACKED = true, oth_replay_rows): game i's position p at row
+//    row_off[i] + p, only rows p <= plies written: the useful bytes alone.
+//    A wave runs only as many bursts as its longest game needs (the strided
+//    layout runs all 17 to zero the rest of the stride), and the block's turn
+//    / end bytes are one contiguous range starting anywhere, staged from its
+//    16-B chunk boundary; the chunks the range shares with the neighbouring
+//    blocks are written byte by byte.
+template <bool PACKED>
 __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict__ start,
                                                         const uint8_t* __restrict__ start_turn,
                                                         const uint8_t* __restrict__ moves,
-                                                        const uint8_t* __restrict__ plies, u64* __restrict__ pos,
+                                                        const uint8_t* __restrict__ plies,
+                                                        const int64_t* __restrict__ row_off, u64* __restrict__ pos,
                                                         uint8_t* __restrict__ pos_turn, uint8_t* __restrict__ pos_end,
                                                         int64_t n, int vec_moves, int vec_out) {
-    extern __shared__ uint4 replay_stage4[];  // kReplayStage bytes when turn or end is wanted
+    extern __shared__ uint4 replay_stage4[];  // the block's packed turn/end bytes when turn or end is wanted
     __shared__ uint4 xrow[kBlock * kXHalf];   // lane-major: lane's 4 rows
     __shared__ unsigned long long xaddr[kBlock];
     __shared__ u32 xmask[kBlock];
@@ -835,11 +881,29 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
     const int nb = (int)min<int64_t>(kBlock, n - blk0);
     const int lane = threadIdx.x;
     const int wl = lane & 63, wbase = lane & ~63;
-    if (staged) {
-        for (int c = lane; c < kReplayStage / 16; c += kBlock) replay_stage4[c] = make_uint4(0, 0, 0, 0);
+    // the block's first output row, and (packed) the 16-B chunk it starts in
+    const int64_t base = PACKED ? row_off[blk0] : blk0 * OTH_POS_STRIDE;
+    const int64_t base_al = PACKED ? (base & ~(int64_t)15) : base;
+    // the block's turn / end bytes: global [base, base + bytes); with row
+    // offsets other than the prefix sum the header asks for, a block whose
+    // range would overrun the LDS stage writes its bytes directly (and a gap
+    // between games is left as the caller had it)
+    int64_t bytes;
+    if (PACKED) {
+        const int64_t last = blk0 + nb - 1;
+        bytes = row_off[last] + min<int>(plies[last], OTH_MOVES_STRIDE) + 1 - base;
+    } else {
+        bytes = (int64_t)nb * OTH_POS_STRIDE;
+    }
+    const int lead = (int)(base - base_al);  // stage bytes before the block's first (packed only)
+    const int64_t span = lead + bytes;
+    const bool direct = PACKED && staged && (bytes < 0 || span > kReplayStagePacked);
+    if (staged && !direct) {  // rows past plies (strided) and any gap (packed) are staged as 0
+        for (int c = lane; c < (PACKED ? kReplayStagePacked : kReplayStage) / 16; c += kBlock)
+            replay_stage4[c] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
-    // every lane of a wave runs the 17 bursts (the exchange is wave-wide);
+    // every lane of a wave runs the wave's bursts (the exchange is wave-wide);
     // a lane past the launch's last game has nothing valid to store
     const bool live = lane < nb;
     const int64_t i = blk0 + (live ? lane : 0);
@@ -857,11 +921,28 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
     else
 #pragma unroll
         for (int j = 0; j < OTH_MOVES_STRIDE / 8; j++) R[j] = 0;
-    ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + i * OTH_POS_STRIDE;
-    uint8_t* st = stage + lane * OTH_POS_STRIDE;
-    const int s = (int)(i & 7);  // the first burst starts at p = -s: whole lines from there on
+    const int64_t row0 = PACKED ? (live ? row_off[i] : base) : i * OTH_POS_STRIDE;
+    ulonglong2* out = reinterpret_cast<ulonglong2*>(pos) + row0;
+    uint8_t* st = stage + (direct ? 0 : row0 - base_al);
+    // the packed turn/end byte of position p: to the stage, or (direct) unpacked
+    // straight to the outputs (the start turn is then written as it is)
+    auto put_te = [&](int p, u32 v, u32 t_full) {
+        if (!direct) {
+            st[p] = (uint8_t)v;
+        } else {
+            if (pos_turn) pos_turn[row0 + p] = (uint8_t)t_full;
+            if (pos_end) pos_end[row0 + p] = (uint8_t)(v >> 7);
+        }
+    };
+    const int s = (int)(row0 & 7);  // the first burst starts at p = -s: whole lines from there on
+    // bursts this wave runs: all 17 (strided), or enough for its longest game
+    int bursts = kReplayBursts;
+    if (PACKED) {
+        bursts = live ? (np + 1 + s + kReplayBurst - 1) / kReplayBurst : 0;
+        for (int off = 32; off >= 1; off >>= 1) bursts = max(bursts, __shfl_xor(bursts, off));
+    }
     u64 prev = 0, cur = R[0];   // move-record words w[b-1], w[b] of burst b
-    for (int bi = 0; bi < kReplayBursts; bi++) {
+    for (int bi = 0; bi < bursts; bi++) {
         const int p0 = 8 * bi - s;
         // move codes p0 .. p0+7 (bytes before position 0 are never used)
         const u64 win = s ? (cur << (8 * s)) | (prev >> (64 - 8 * s)) : cur;
@@ -884,7 +965,7 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                     analyse(P, O, pm);
                     u32 e = 0;
                     if (pm.legal == 0) e = moves_of(O, P) == 0;
-                    st[p] = (uint8_t)(t | (e << 7));
+                    put_te(p, t | (e << 7), t);
                     if (p < np) {
                         if (c == OTH_PASS) {
                             t ^= 3u;
@@ -904,7 +985,7 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                 if (staged) {
                     u32 e = 0;
                     if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
-                    st[p] = (uint8_t)(min(t, kTurnEscape) | (e << 7));
+                    put_te(p, min(t, kTurnEscape) | (e << 7), t);
                 }
                 // put_s semantics (board.py:192-209): pass toggles; illegal leaves the state
                 if (p < np && !fast) {
@@ -941,7 +1022,7 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                 const int p = p0 + h * kXHalf + k;
                 const ulonglong2 v = b[h * kXHalf + k];
                 xrow[lane * kXHalf + k] = make_uint4((u32)v.x, (u32)(v.x >> 32), (u32)v.y, (u32)(v.y >> 32));
-                valid |= (live && p >= 0 && p < OTH_POS_STRIDE ? 1u : 0u) << k;
+                valid |= (live && p >= 0 && p < (PACKED ? np + 1 : OTH_POS_STRIDE) ? 1u : 0u) << k;
             }
             xaddr[lane] = reinterpret_cast<unsigned long long>(out + (p0 + h * kXHalf));
             xmask[lane] = valid;
@@ -960,13 +1041,25 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
         R[OTH_MOVES_STRIDE / 8 - 1] = 0;
         cur = R[0];
     }
-    if (!staged) return;
+    if (!staged || direct) return;
     __syncthreads();
-    // the block's rows of pos_turn / pos_end are one contiguous range each
-    const int bytes = nb * OTH_POS_STRIDE;
-    const int64_t base = blk0 * OTH_POS_STRIDE;
+    // the block's rows of pos_turn / pos_end are one contiguous range each:
+    // global bytes [base, base + bytes), staged from base_al
+    // the game of a staged byte (the escape path only): by division, or by a
+    // search of the block's row offsets
+    auto game_of = [&](int64_t q) -> int64_t {
+        if (!PACKED) return blk0 + q / OTH_POS_STRIDE;
+        const int64_t row = base_al + q;
+        int lo = 0, hi = nb - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (row_off[blk0 + mid] <= row) lo = mid;
+            else hi = mid - 1;
+        }
+        return blk0 + lo;
+    };
     if (vec_out) {
-        for (int c = lane; c * 16 < bytes; c += kBlock) {
+        for (int c = lane; c * 16 < span; c += kBlock) {
             const uint4 v = replay_stage4[c];
             u32 w[4] = {v.x, v.y, v.z, v.w};
             u32 tw[4], ew[4];
@@ -977,31 +1070,36 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                 ew[q] = (w[q] >> 7) & 0x01010101u;
                 esc |= ((tw[q] + 0x01010101u) & 0x80808080u) != 0;  // a byte == 0x7f
             }
+            const int64_t q0 = (int64_t)c * 16;
             if (esc) {  // rare: a start turn >= 127 still to move
-#pragma unroll
+#pragma unroll 1
                 for (int q = 0; q < 16; q++) {
-                    const int o = c * 16 + q;
+                    if (q0 + q < lead || q0 + q >= span) continue;
+                    const u32 byte = w[q >> 2] >> (8 * (q & 3)) & 0xffu;
+                    if ((byte & kTurnEscape) != kTurnEscape) continue;
                     uint8_t tb, eb;
-                    unstage_byte(w[q >> 2] >> (8 * (q & 3)) & 0xffu, start_turn, blk0 + o / OTH_POS_STRIDE, tb, eb);
+                    unstage_byte(byte, start_turn, game_of(q0 + q), tb, eb);
                     tw[q >> 2] = (tw[q >> 2] & ~(0xffu << (8 * (q & 3)))) | ((u32)tb << (8 * (q & 3)));
                 }
             }
-            if ((c + 1) * 16 <= bytes) {
-                if (pos_turn) *reinterpret_cast<uint4*>(pos_turn + base + c * 16) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
-                if (pos_end) *reinterpret_cast<uint4*>(pos_end + base + c * 16) = make_uint4(ew[0], ew[1], ew[2], ew[3]);
-            } else {  // the launch's last partial chunk
-                for (int q = 0; c * 16 + q < bytes; q++) {
-                    if (pos_turn) pos_turn[base + c * 16 + q] = (uint8_t)(tw[q >> 2] >> (8 * (q & 3)));
-                    if (pos_end) pos_end[base + c * 16 + q] = (uint8_t)(ew[q >> 2] >> (8 * (q & 3)));
+            const int64_t g0 = base_al + q0;  // global byte of the chunk's first
+            if (q0 >= lead && q0 + 16 <= span) {
+                if (pos_turn) *reinterpret_cast<uint4*>(pos_turn + g0) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+                if (pos_end) *reinterpret_cast<uint4*>(pos_end + g0) = make_uint4(ew[0], ew[1], ew[2], ew[3]);
+            } else {  // a chunk the range shares with a neighbour, or the launch's last
+                for (int q = 0; q < 16; q++) {
+                    if (q0 + q < lead || q0 + q >= span) continue;
+                    if (pos_turn) pos_turn[g0 + q] = (uint8_t)(tw[q >> 2] >> (8 * (q & 3)));
+                    if (pos_end) pos_end[g0 + q] = (uint8_t)(ew[q >> 2] >> (8 * (q & 3)));
                 }
             }
         }
     } else {  // a caller's output that is not 16-B aligned: coalesced byte stores
-        for (int o = lane; o < bytes; o += kBlock) {
+        for (int64_t o = lead + lane; o < span; o += kBlock) {
             uint8_t tb, eb;
-            unstage_byte(stage[o], start_turn, blk0 + o / OTH_POS_STRIDE, tb, eb);
-            if (pos_turn) pos_turn[base + o] = tb;
-            if (pos_end) pos_end[base + o] = eb;
+            unstage_byte(stage[o], start_turn, game_of(o), tb, eb);
+            if (pos_turn) pos_turn[base_al + o] = tb;
+            if (pos_end) pos_end[base_al + o] = eb;
         }
     }
 }
@@ -1152,8 +1250,11 @@ __device__ __forceinline__ int64_t td_key(ulonglong2 b, u32 sd) {
     return (int64_t)k;
 }
 
-// one thread per recorded position (g, p)
+// one thread per recorded position (g, p); rows of an oth_replay table
+// (row_off == nullptr: row g*OTH_POS_STRIDE + p) or of an oth_replay_rows one
+// (row row_off[g] + p)
 __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restrict__ pos,
+                                                            const int64_t* __restrict__ row_off,
                                                             const uint8_t* __restrict__ plies,
                                                             const int64_t* __restrict__ base,
                                                             const double* __restrict__ lam_pow,
@@ -1165,7 +1266,7 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     const u32 p = (u32)(idx - g * OTH_POS_STRIDE);
     const u32 np = min<u32>(plies[g], OTH_MOVES_STRIDE);
     if (p > np) return;
-    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + g * OTH_POS_STRIDE;
+    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + (row_off ? row_off[g] : g * OTH_POS_STRIDE);
     const ulonglong2 term = row[np];
     const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
     const ulonglong2 b = row[p];
@@ -1548,10 +1649,19 @@ int oth_result(const uint64_t* boards, uint8_t* n_black, uint8_t* n_white, int8_
 }
 
 namespace {
+struct RunnerSpec {
+    int n_rand_a, n_rand_b, swap;
+    uint8_t* a_black;
+};
 int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
                    int n_random, const int8_t* w_black, const int8_t* w_white, uint64_t* final_boards, int8_t* diff,
-                   uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream) {
+                   uint8_t* plies, uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream,
+                   const RunnerSpec* run = nullptr) {
     RolloutArgs a;
+    a.n_rand_a = run ? (u32)std::min(run->n_rand_a, 10) : 0u;  // N_RAND_HAND_UNTIL (game_runner.py:6, 117-118)
+    a.n_rand_b = run ? (u32)std::min(run->n_rand_b, 10) : 0u;
+    a.swap = run ? run->swap : 0;
+    a.a_black = run ? run->a_black : nullptr;
     a.start = start;
     a.start_turn = start_turn;
     a.seed_state = mix64(seed + GOLDEN64);
@@ -1580,7 +1690,15 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     a.coop_cap = (u32)std::min(std::max(env_int("OTH_COOP_CAP", kCoopCap), 0), kCoopCap);
     a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
     hipStream_t st = (hipStream_t)stream;
-    if (policy == OTH_POLICY_EVAL) {
+    if (run) {
+        if (policy == OTH_POLICY_EVAL) {
+            if (moves) rollout_kernel<OTH_POLICY_EVAL, true, true><<<grid, kBlock, 0, st>>>(a);
+            else rollout_kernel<OTH_POLICY_EVAL, false, true><<<grid, kBlock, 0, st>>>(a);
+        } else {
+            if (moves) rollout_kernel<OTH_POLICY_GREEDY, true, true><<<grid, kBlock, 0, st>>>(a);
+            else rollout_kernel<OTH_POLICY_GREEDY, false, true><<<grid, kBlock, 0, st>>>(a);
+        }
+    } else if (policy == OTH_POLICY_EVAL) {
         if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_EVAL, false><<<grid, kBlock, 0, st>>>(a);
     } else if (policy == OTH_POLICY_GREEDY) {
@@ -1622,6 +1740,19 @@ int oth_rollout_match(const uint64_t* start, const uint8_t* start_turn, uint64_t
                           final_boards, diff, plies, moves, hist, work, n, stream);
 }
 
+int oth_rollout_runner(const uint64_t* start, const uint8_t* start_turn, uint64_t seed, uint64_t game_id0, int policy,
+                       const int8_t* weights_a, const int8_t* weights_b, int n_rand_a, int n_rand_b, int swap_colours,
+                       uint8_t* a_black, uint64_t* final_boards, int8_t* diff, uint8_t* plies, uint8_t* moves,
+                       int64_t* hist, uint64_t* work, int64_t n, void* stream) {
+    if (n < 0 || !work || (policy != OTH_POLICY_GREEDY && policy != OTH_POLICY_EVAL) ||
+        (policy == OTH_POLICY_EVAL && (!weights_a || !weights_b)) || n_rand_a < 0 || n_rand_b < 0)
+        return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    const RunnerSpec run{n_rand_a, n_rand_b, swap_colours != 0, a_black};
+    return rollout_launch(start, start_turn, seed, game_id0, policy, 0, weights_a, weights_b, final_boards, diff,
+                          plies, moves, hist, work, n, stream, &run);
+}
+
 int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
                uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!moves || !plies || !pos_boards))) return OTH_EINVAL;
@@ -1629,10 +1760,24 @@ int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* 
     const bool staged = pos_turn || pos_end;
     const int vec_moves = ((uintptr_t)moves & 15) == 0;
     const int vec_out = (((uintptr_t)pos_turn | (uintptr_t)pos_end) & 15) == 0;
-    replay_kernel<<<blocks_for(n), kBlock, staged ? kReplayStage : 0, (hipStream_t)stream>>>(
-        start, start_turn, moves, plies, pos_boards, pos_turn, pos_end, n, vec_moves, vec_out);
+    replay_kernel<false><<<blocks_for(n), kBlock, staged ? kReplayStage : 0, (hipStream_t)stream>>>(
+        start, start_turn, moves, plies, nullptr, pos_boards, pos_turn, pos_end, n, vec_moves, vec_out);
     return launched();
 }
+
+int oth_replay_rows(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
+                    const int64_t* row_off, uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n,
+                    void* stream) {
+    if (n < 0 || (n > 0 && (!moves || !plies || !row_off || !pos_boards))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    const bool staged = pos_turn || pos_end;
+    const int vec_moves = ((uintptr_t)moves & 15) == 0;
+    const int vec_out = (((uintptr_t)pos_turn | (uintptr_t)pos_end) & 15) == 0;
+    replay_kernel<true><<<blocks_for(n), kBlock, staged ? kReplayStagePacked : 0, (hipStream_t)stream>>>(
+        start, start_turn, moves, plies, row_off, pos_boards, pos_turn, pos_end, n, vec_moves, vec_out);
+    return launched();
+}
+
 
 int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream) {
     if (n < 0 || (n > 0 && (!boards || !turn || !out))) return OTH_EINVAL;
@@ -1664,8 +1809,20 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
                    int64_t* keys, double* values, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, plies, base,
-                                                                                          lam_pow, keys, values, n);
+    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, nullptr, plies,
+                                                                                          base, lam_pow, keys, values,
+                                                                                          n);
+    return launched();
+}
+
+int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
+                        const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!pos_boards || !row_off || !plies || !base || !lam_pow || !keys || !values)))
+        return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, row_off, plies,
+                                                                                          base, lam_pow, keys, values,
+                                                                                          n);
     return launched();
 }
 

@@ -13,8 +13,12 @@ policy into GameRunner unchanged:
                    the move ('d3', 'ps', ...) is applied for the side to move
                    (go_for also sends the engine its OWN randomised moves, 149)
   verbose p     -> 1 line (parameter description)           (game_runner.py:66-73)
-  verbose 1     -> 13 lines of board display                 (game_runner.py:75-91)
-  verbose 0     -> nothing
+  verbose 1     -> 13 lines: the board display, the last line "Black won" /
+                   "White won" once the game is over with a winner
+                   (Player.show parses "(Black|White) won", game_runner.py:75-91)
+  verbose 0     -> after a "verbose 1": 1 line, "Game Over" once the game is
+                   over (Player.show reads one line and looks for it, 92-95);
+                   otherwise nothing (show_hamlet_param sends it unread, 70)
   quit          -> 1 line, exit                              (game_runner.py:56-64)
 
 Rules and move generation run on the GPU through the drop-in Board
@@ -44,6 +48,7 @@ class Engine:
         self.rng = random.Random(seed)
         self.weights = params.as_weights(params.DEFAULT_WEIGHTS if weights is None else weights)
         self.board = gboard.Board()
+        self._shown = False  # a "verbose 1" awaits its "verbose 0" line
 
     def _children(self, puts, want_legal):
         """Every child of the side to move in ONE oth_step launch (board
@@ -100,12 +105,21 @@ class Engine:
             extra = " weights=%s" % self.weights.reshape(-1).tolist() if self.policy == "eval" else ""
             out("%s policy=%s%s" % (self.name, self.policy, extra))
         elif cmd == "verbose 1":
-            text = str(self.board).rstrip("\n").split("\n")
-            text += [""] * (13 - len(text))
-            for t in text[:13]:
+            b = self.board
+            text = str(b).rstrip("\n").split("\n")[:12]
+            text += [""] * (12 - len(text))
+            won = ""
+            if b.is_game_over() and b.n_black() != b.n_white():
+                won = "Black won" if b.n_black() > b.n_white() else "White won"
+            for t in text + [won]:
                 out(t)
+            self._shown = True
+        elif cmd == "verbose 0":
+            if self._shown:
+                out("Game Over" if self.board.is_game_over() else "")
+            self._shown = False
         elif cmd.startswith("verbose"):
-            pass
+            self._shown = False
         elif cmd == "quit":
             out("bye")
             return False

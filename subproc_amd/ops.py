@@ -32,6 +32,7 @@ Result = namedtuple("Result", "n_black n_white diff terminal")
 RolloutResult = namedtuple("RolloutResult", "final_boards diff plies moves hist")
 Positions = namedtuple("Positions", "boards turn nturn move")
 Replay = namedtuple("Replay", "boards turn end")
+ReplayRows = namedtuple("ReplayRows", "boards turn end row_off")
 
 _POLICIES = {"random": POLICY_RANDOM, "greedy": POLICY_GREEDY, "eval": POLICY_EVAL, POLICY_RANDOM: POLICY_RANDOM,
              POLICY_GREEDY: POLICY_GREEDY, POLICY_EVAL: POLICY_EVAL}
@@ -210,6 +211,10 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     """
     if policy not in _POLICIES:
         raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
+    capturing = torch.cuda.is_current_stream_capturing()
+    if work is None and capturing:
+        raise RuntimeError("ops.rollout under graph capture needs an explicit work word: an int64 (1,) device "
+                           "tensor zeroed before the capture, one per captured launch")
     d = _device(device) if start is None else start.device
     ps = pst = None
     if start is not None:
@@ -226,10 +231,6 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
     if _POLICIES[policy] != POLICY_EVAL and (weights is not None or weights_white is not None):
         raise ValueError("weights apply to policy 'eval' only")
-    capturing = torch.cuda.is_current_stream_capturing()
-    if work is None and capturing:
-        raise RuntimeError("ops.rollout under graph capture needs an explicit work word: an int64 (1,) device "
-                           "tensor zeroed before the capture, one per captured launch")
     w = work_word(d) if work is None else work
     pw = _dev(w, "work", torch.int64, (1,), d)
 
@@ -259,6 +260,55 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
                 w.zero_()
         check(rc, what)
     return RolloutResult(fb, df, pl, mv, hist)
+
+
+RunnerResult = namedtuple("RunnerResult", "final_boards diff plies moves hist a_black")
+
+
+def rollout_runner(n, seed, game_id0=0, policy="eval", weights_a=None, weights_b=None, n_rand_a=0, n_rand_b=0,
+                   swap_colours=False, start=None, start_turn=None, record_moves=False, hist=None, device="cuda",
+                   work=None):
+    """n GameRunner matches between player A and player B on the GPU
+    (oth_rollout_runner, include/othello.h): both play ``policy`` ("greedy",
+    or "eval" with tables ``weights_a`` / ``weights_b``, default
+    params.DEFAULT_WEIGHTS), each places min(n_rand, 10) random moves by
+    go_for's coin (game_runner.py:115-150), and with ``swap_colours`` each game
+    draws who plays Black (subproc.do_match's proc_randomize_black_white).
+    Game i is global id game_id0 + i.  ``a_black`` (n,) uint8: 1 where A
+    played Black; diff / hist / final boards are by colour."""
+    if policy not in ("greedy", "eval"):
+        raise ValueError(f"policy must be 'greedy' or 'eval', got {policy!r}")
+    if work is None and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ops.rollout_runner under graph capture needs an explicit work word")
+    d = _device(device) if start is None else start.device
+    ps = pst = None
+    if start is not None:
+        if _n(start) != n:
+            raise ValueError("start must have n rows")
+        ps = _dev(start, "start", torch.int64)
+        pst = _opt(start_turn, "start_turn", torch.uint8, (n,), start.device)
+    fb = torch.empty((n, 2), dtype=torch.int64, device=d)
+    df = torch.empty(n, dtype=torch.int8, device=d)
+    pl = torch.empty(n, dtype=torch.uint8, device=d)
+    ab = torch.empty(n, dtype=torch.uint8, device=d)
+    mv = torch.empty((n, MOVES_STRIDE), dtype=torch.uint8, device=d) if record_moves else None
+    if hist is None:
+        hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=d)
+    ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
+    w = work_word(d) if work is None else work
+    pw = _dev(w, "work", torch.int64, (1,), d)
+    with torch.cuda.device(d):
+        rc = _lib.load().oth_rollout_runner(ps, pst, seed & (2**64 - 1), game_id0, _POLICIES[policy],
+                                            _weights_ptr(weights_a), _weights_ptr(weights_b), int(n_rand_a),
+                                            int(n_rand_b), int(bool(swap_colours)), ab.data_ptr(), fb.data_ptr(),
+                                            df.data_ptr(), pl.data_ptr(), None if mv is None else mv.data_ptr(), ph,
+                                            pw, n, _stream())
+        if rc != _lib.OTH_OK and work is not None and not torch.cuda.is_current_stream_capturing():
+            w.zero_()
+        elif rc != _lib.OTH_OK:
+            _WORK.pop((d.index, torch.cuda.current_stream().cuda_stream), None)
+        check(rc, "oth_rollout_runner")
+    return RunnerResult(fb, df, pl, mv, hist, ab)
 
 
 def sample_midgame(n, seed, index0=0, device="cuda"):
@@ -294,6 +344,37 @@ def replay(moves, plies, start=None, start_turn=None):
         check(_lib.load().oth_replay(ps, pst, pm, pp, b.data_ptr(), t.data_ptr(), e.data_ptr(), n, _stream()),
               "oth_replay")
     return Replay(b, t, e)
+
+
+def row_offsets(plies):
+    """Exclusive prefix sum of min(plies, 128) + 1 (int64, on plies' device):
+    the first row of each game in an oth_replay_rows table; also returns the
+    total row count (one host sync)."""
+    cnt = plies.long().clamp(max=MOVES_STRIDE) + 1
+    ends = torch.cumsum(cnt, 0)
+    total = int(ends[-1]) if ends.numel() else 0
+    return (ends - cnt).contiguous(), total
+
+
+def replay_rows(moves, plies, start=None, start_turn=None):
+    """ops.replay into packed rows (oth_replay_rows): game i's recorded
+    positions are rows row_off[i] .. row_off[i] + plies[i] of boards (R, 2)
+    int64, turn (R,) and end (R,) uint8, R = sum(plies + 1) -- only the rows
+    GameRunner records, about half of the strided table of random games."""
+    n = moves.shape[0]
+    pm = _dev(moves, "moves", torch.uint8, (n, MOVES_STRIDE))
+    pp = _dev(plies, "plies", torch.uint8, (n,), moves.device)
+    ps = _opt(start, "start", torch.int64, (n, 2), moves.device)
+    pst = _opt(start_turn, "start_turn", torch.uint8, (n,), moves.device)
+    dev = moves.device
+    row_off, total = row_offsets(plies)
+    b = torch.empty((total, 2), dtype=torch.int64, device=dev)
+    t = torch.empty(total, dtype=torch.uint8, device=dev)
+    e = torch.empty(total, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        check(_lib.load().oth_replay_rows(ps, pst, pm, pp, row_off.data_ptr(), b.data_ptr(), t.data_ptr(),
+                                          e.data_ptr(), n, _stream()), "oth_replay_rows")
+    return ReplayRows(b, t, e, row_off)
 
 
 def book_text(boards, turn):

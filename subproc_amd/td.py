@@ -97,12 +97,17 @@ class StateMap:
     def __len__(self):
         return int(self.keys.numel())
 
-    def update(self, pos_boards, plies):
+    def update(self, pos_boards, plies, row_off=None):
         """Apply the books of n games: pos_boards (n, 129, 2) int64 as ops.replay
-        returns it, plies (n,) uint8.  Returns the number of updates applied."""
+        returns it, or the packed (R, 2) rows of ops.replay_rows with their
+        ``row_off``; plies (n,) uint8.  Returns the number of updates applied."""
         n = plies.shape[0]
-        if pos_boards.shape != (n, POS_STRIDE, 2) or pos_boards.dtype != torch.int64:
-            raise ValueError("pos_boards must be an (n, 129, 2) int64 replay table")
+        if row_off is None:
+            if pos_boards.shape != (n, POS_STRIDE, 2) or pos_boards.dtype != torch.int64:
+                raise ValueError("pos_boards must be an (n, 129, 2) int64 replay table")
+        elif pos_boards.dim() != 2 or pos_boards.shape[1] != 2 or pos_boards.dtype != torch.int64 or \
+                row_off.shape != (n,) or row_off.dtype != torch.int64 or row_off.device != self.device:
+            raise ValueError("packed rows: pos_boards (R, 2) int64 and row_off (n,) int64 on the map's device")
         if plies.dtype != torch.uint8 or pos_boards.device != self.device or plies.device != self.device:
             raise ValueError("plies must be uint8; both on the map's device")
         if n == 0:
@@ -116,9 +121,15 @@ class StateMap:
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            check(lib.oth_td_updates(pos_boards.contiguous().data_ptr(), plies.contiguous().data_ptr(),
-                                     base.data_ptr(), self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n,
-                                     stream), "oth_td_updates")
+            if row_off is None:
+                check(lib.oth_td_updates(pos_boards.contiguous().data_ptr(), plies.contiguous().data_ptr(),
+                                         base.data_ptr(), self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(),
+                                         n, stream), "oth_td_updates")
+            else:
+                check(lib.oth_td_updates_rows(pos_boards.contiguous().data_ptr(), row_off.contiguous().data_ptr(),
+                                              plies.contiguous().data_ptr(), base.data_ptr(),
+                                              self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n, stream),
+                      "oth_td_updates_rows")
             sk, sv = torch.empty_like(keys), torch.empty_like(vals)
             tb = ctypes.c_size_t(0)
             check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total, None,
@@ -170,7 +181,7 @@ class StateMap:
 
     def update_from_books(self, books):
         """Apply a subproc_amd.books.GameBooks batch."""
-        return self.update(books.pos.boards, books.plies)
+        return self.update(books.pos.boards, books.plies, books.pos.row_off)
 
     def get(self, counts):
         """Value for a counts() tuple, 0.0 if absent (a fresh key reads as 0, 53-56)."""

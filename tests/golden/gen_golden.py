@@ -234,6 +234,92 @@ def play(args):
     return moves, fb, fw, b.n_black() - b.n_white(), ply
 
 
+def policy_move(b, policy, weights):
+    """The 1-ply policies of play() for the side to move (a legal move exists)."""
+    best, bestv = None, None
+    for (x, y) in b.puttables(b.turn):
+        c = clone(b)
+        assert c.put_s(c.handstr_from_coord(x, y)) > 0
+        if policy == 1:
+            v = -c.n_puttable_for(hostile(b.turn))
+        else:
+            v = eval_value(c, "O" if b.turn == Black else "X", weights)
+        if bestv is None or v > bestv:
+            best, bestv = x + 8 * y, v
+    return best
+
+
+def play_runner(args):
+    """One GameRunner match (game_runner.py:104-201 as subproc.do_match runs
+    it, subproc.py:15-39) between player A and player B, both playing
+    `policy` (1 greedy, 2 eval with their own tables), driven through board.py.
+    The reference draws with Python's random; here the same decisions draw
+    from the game's counter stream, in the same order:
+      * do_match: with randomize_black_white, randrange(2) == 1 swaps A and B
+        (A then plays White) -> pick(2) == 1;
+      * GameRunner.__init__: n_rand_rest = min(n_rand_hands, N_RAND_HAND_UNTIL);
+      * go_for, on every turn of a player with n_rand_rest > 0 (passes
+        included): randrange(n_rand_rest) == 0 -> pick(r) == 0; then if
+        puttables is not empty, puttables[randrange(len)] -> pick(len) and
+        n_rand_rest -= 1; otherwise the engine's own move (the policy), or PS.
+    """
+    seed, g, policy, wa, wb, n_rand_a, n_rand_b, swap, bl, wh, turn = args
+    rng = GameRng(game_key(seed_state(seed), g))
+    a_black = not (swap and rng.pick(2) == 1)
+    ra, rb = min(n_rand_a, 10), min(n_rand_b, 10)
+    players = {Black: {"w": wa if a_black else wb, "rest": ra if a_black else rb},
+               White: {"w": wb if a_black else wa, "rest": rb if a_black else ra}}
+    b = from_bits(bl, wh, turn)
+    moves = []
+    while not b.is_game_over():
+        pl = players[b.turn]
+        code = None
+        if pl["rest"] > 0 and rng.pick(pl["rest"]) == 0:
+            puts = b.puttables(b.turn)
+            if len(puts) > 0:
+                x, y = puts[rng.pick(len(puts))]
+                code = x + 8 * y
+                pl["rest"] -= 1
+        if code is None:
+            code = policy_move(b, policy, pl["w"]) if b.puttables(b.turn) else PASS
+        assert b.put_s(code_to_str(b, code)) >= 0
+        moves.append(code)
+    fb, fw = to_bits(b)
+    return moves, fb, fw, b.n_black() - b.n_white(), len(moves), int(a_black)
+
+
+def runner_fixtures(pool):
+    """rollout_runner_*.npz: GameRunner matches (play_runner) through board.py."""
+    ib, iw = to_bits(Board())
+    ns = load_reference_counts(want_ns=True)
+    wdef = [list(r) for r in ns["ProgressPositionMovesParameter"]().default_value()]
+    wrand = np.random.default_rng(77).integers(-127, 128, (4, 9)).tolist()
+    mid = [(p[0], p[1], p[2]) for p in random_positions(256, 20240601) if p[2] in (Black, White)][:48]
+
+    def runner(name, seed, g0, n, policy, wa, wb, n_rand_a, n_rand_b, swap, starts=None):
+        starts = starts or [(ib, iw, Black)] * n
+        args = [(seed, g0 + i, policy, wa, wb, n_rand_a, n_rand_b, swap, *st) for i, st in enumerate(starts)]
+        res = pool.map(play_runner, args, chunksize=4)
+        mv = np.full((n, 128), 255, np.uint8)
+        for i, r in enumerate(res):
+            mv[i, :len(r[0])] = r[0]
+        np.savez_compressed(
+            os.path.join(OUT, name + ".npz"),
+            seed=np.array(seed, np.uint64), game_id0=np.array(g0, np.uint64), policy=np.array(policy),
+            n_rand_a=np.array(n_rand_a), n_rand_b=np.array(n_rand_b), swap=np.array(int(swap)),
+            start_black=u64([s[0] for s in starts]), start_white=u64([s[1] for s in starts]),
+            start_turn=np.array([s[2] for s in starts], np.uint8),
+            moves=mv, final_black=u64([r[1] for r in res]), final_white=u64([r[2] for r in res]),
+            diff=np.array([r[3] for r in res], np.int8), plies=np.array([r[4] for r in res], np.uint8),
+            a_black=np.array([r[5] for r in res], np.uint8),
+            weights_a=np.array(wa if wa is not None else [[0] * 9] * 4, np.int8),
+            weights_b=np.array(wb if wb is not None else [[0] * 9] * 4, np.int8))
+
+    runner("rollout_runner_eval", 6161, 40, 128, 2, wdef, wrand, 10, 3, True)
+    runner("rollout_runner_greedy", 6262, 1 << 33, 96, 1, None, None, 4, 0, False)
+    runner("rollout_runner_eval_mid", 6363, 7, len(mid), 2, wrand, wdef, 25, 7, True, starts=mid)
+
+
 # learner shards of the disc count (ProgressPositionMovesLearn.__get_fit_parameters_shards,
 # progress_position_moves_learn.py:112-113; that module needs pyres/slack, so the
 # four bounds are restated here)
@@ -599,6 +685,7 @@ def main():
     rollouts("rollout_eval_rand_from_mid", 4242, 77, 64, 2, 0, starts=mid[:64], weights=wrand)
     # a match: the reference's default table as Black against the random table as White
     rollouts("rollout_match", 5150, 9, 128, 2, 6, weights=wdef, weights_white=wrand)
+    runner_fixtures(pool)
     boards = [from_bits(p[0], p[1], p[2]) for p in pos[:512]]
     np.savez_compressed(
         os.path.join(OUT, "eval_values.npz"),
@@ -840,7 +927,11 @@ def batch_stats_fixtures():
 
 
 if __name__ == "__main__":
-    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "batch_stats":
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only == "batch_stats":
         batch_stats_fixtures()
+    elif only == "runner":
+        runner_fixtures(mp.Pool(8))
+        print("runner fixtures written to", OUT)
     else:
         main()

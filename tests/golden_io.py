@@ -24,3 +24,5 @@ def h(x):
 
 ROLLOUT_FIXTURES = ["rollout_random", "rollout_random_offset", "rollout_random_from_mid", "rollout_greedy",
                     "rollout_greedy_from_mid", "rollout_eval", "rollout_eval_rand_from_mid", "rollout_match"]
+
+RUNNER_FIXTURES = ["rollout_runner_eval", "rollout_runner_greedy", "rollout_runner_eval_mid"]

@@ -147,3 +147,29 @@ def test_sample_midgame_fixture_and_einval():
     assert lib().oth_rollout(None, None, 1, 0, 0, 0, None, None, None, None, None, None, 4, None) == _lib.OTH_EINVAL
     assert lib().oth_step(None, None, None, None, None, None, None, None, None, 3, None) == _lib.OTH_EINVAL
     assert lib().oth_eval(None, None, None, None, 0, None) == _lib.OTH_EINVAL
+
+
+@pytest.mark.parametrize("name", ["rollout_runner_eval", "rollout_runner_greedy", "rollout_runner_eval_mid"])
+def test_rollout_runner_fixtures(name):
+    z = load_npz(name + ".npz")
+    n = len(z["plies"])
+    st = boards(z["start_black"], z["start_white"])
+    stt = np.ascontiguousarray(z["start_turn"])
+    wa, wb = (ctypes.c_int8 * 36)(*z["weights_a"].reshape(-1).tolist()), (ctypes.c_int8 * 36)(*z["weights_b"].reshape(-1).tolist())
+    fb, d, pl, ab = np.zeros((n, 2), np.uint64), np.zeros(n, np.int8), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    mv, hist = np.zeros((n, 128), np.uint8), np.zeros(133, np.int64)
+    rc = lib().oth_rollout_runner(P(st), P(stt), int(z["seed"]), int(z["game_id0"]), int(z["policy"]), wa, wb,
+                                  int(z["n_rand_a"]), int(z["n_rand_b"]), int(z["swap"]), P(ab), P(fb), P(d), P(pl),
+                                  P(mv), P(hist), P(WORK), n, None)
+    assert rc == 0
+    np.testing.assert_array_equal(mv, z["moves"])
+    np.testing.assert_array_equal(ab, z["a_black"])
+    np.testing.assert_array_equal(fb, boards(z["final_black"], z["final_white"]))
+    assert int(hist[132]) == int(z["plies"].astype(np.int64).sum())
+    E = _lib.OTH_EINVAL
+    assert lib().oth_rollout_runner(None, None, 1, 0, 0, wa, wb, 0, 0, 0, None, None, None, None, None, None, P(WORK),
+                                    4, None) == E  # random is not a runner policy
+    assert lib().oth_rollout_runner(None, None, 1, 0, 2, None, wb, 0, 0, 0, None, None, None, None, None, None,
+                                    P(WORK), 4, None) == E
+    assert lib().oth_rollout_runner(None, None, 1, 0, 1, None, None, -1, 0, 0, None, None, None, None, None, None,
+                                    P(WORK), 4, None) == E

@@ -197,6 +197,23 @@ def test_rollout_pair(policy):
     assert int(wk.d.item()) == 0  # every launch leaves its work word at 0
 
 
+@pytest.mark.parametrize("policy", [1, 2])
+def test_rollout_runner_pair(policy):
+    n = 4096
+    b, t, _, _ = positions(n, 5)
+    wa = (ctypes.c_int8 * 36)(*np.random.default_rng(11).integers(-127, 128, 36).tolist())
+    wb = (ctypes.c_int8 * 36)(*np.random.default_rng(12).integers(-127, 128, 36).tolist())
+    outs = [Buf(np.zeros(n, np.uint8)), Buf(np.zeros((n, 2), np.uint64)), Buf(np.zeros(n, np.int8)),
+            Buf(np.zeros(n, np.uint8)), Buf(np.zeros((n, _lib.MOVES_STRIDE), np.uint8)),
+            Buf(np.zeros(_lib.HIST_BINS, np.int64))]
+    wk = work()
+    both("oth_rollout_runner", None, None, 31, 1 << 29, policy, wa, wb, 10, 3, 1, *outs, wk, n)
+    same(*outs)
+    both("oth_rollout_runner", b, t, 32, 9, policy, wa, wb, 2, 12, 0, *outs, wk, n)  # mid-game starts, no swap
+    same(*outs)
+    assert int(wk.d.item()) == 0
+
+
 def test_books_features_eval_pair():
     n = 512
     outs = [None, None, Buf(np.zeros(n, np.uint8)), Buf(np.full((n, _lib.MOVES_STRIDE), 255, np.uint8)), None]
@@ -207,6 +224,12 @@ def test_books_features_eval_pair():
     both("oth_replay", None, None, outs[3], outs[2], pos, pt, pe, n)
     # every row is written by both: board, turn and end rows past plies as 0
     same(pos, pt, pe)
+    rows = outs[2].h.astype(np.int64) + 1
+    off = Buf(np.cumsum(rows) - rows)
+    pk = [Buf(np.zeros((int(rows.sum()), 2), np.uint64)), Buf(np.zeros(int(rows.sum()), np.uint8)),
+          Buf(np.zeros(int(rows.sum()), np.uint8))]
+    both("oth_replay_rows", None, None, outs[3], outs[2], off, *pk, n)
+    same(*pk)
     past = np.arange(_lib.POS_STRIDE)[None, :] > outs[2].h[:, None]
     assert (pos.h[past] == 0).all() and (pt.h[past] == 0).all() and (pe.h[past] == 0).all()
     k = n * _lib.POS_STRIDE
@@ -240,6 +263,17 @@ def test_td_pair():
     keys, vals = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
     both("oth_td_updates", pos, plies, base, lam, keys, vals, n)
     same(keys, vals)
+    # the packed-rows layout: oth_replay_rows + oth_td_updates_rows give the same stream
+    rows = plies.h.astype(np.int64) + 1
+    off = Buf(np.cumsum(rows) - rows)
+    prow = Buf(np.zeros((int(rows.sum()), 2), np.uint64))
+    both("oth_replay_rows", None, None, moves, plies, off, prow, None, None, n)
+    same(prow)
+    keys2, vals2 = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+    both("oth_td_updates_rows", prow, off, plies, base, lam, keys2, vals2, n)
+    same(keys2, vals2)
+    np.testing.assert_array_equal(keys2.h, keys.h)
+    np.testing.assert_array_equal(vals2.h.view(np.int64), vals.h.view(np.int64))
     order = np.argsort(keys.h, kind="stable")
     uk, starts = np.unique(keys.h[order], return_index=True)
     sv = Buf(vals.h[order])
@@ -279,6 +313,13 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_rollout_match(None, None, 1, 0, 0, w, w, None, None, None, None, None, W, 0, s) == 0
         assert lib.oth_hands(None, None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_replay(None, None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_replay_rows(None, None, None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_replay_rows(None, None, None, None, None, None, None, None, 3, s) == _lib.OTH_EINVAL
+        assert lib.oth_td_updates_rows(None, None, None, None, None, None, None, 0, s) == 0
+        assert lib.oth_rollout_runner(None, None, 1, 0, 1, None, None, 0, 0, 0, None, None, None, None, None, None,
+                                      W, 0, s) == 0
+        assert lib.oth_rollout_runner(None, None, 1, 0, 0, w, w, 0, 0, 0, None, None, None, None, None, None,
+                                      W, 5, s) == _lib.OTH_EINVAL  # random is not a runner policy
         assert lib.oth_book_text(None, None, 0, None, s) == 0
         assert lib.oth_features(None, None, None, 0, s) == 0
         assert lib.oth_eval(None, None, w, None, 0, s) == 0

@@ -59,3 +59,53 @@ def test_bench_dist_secondary_step_lines_one_rank():
         s = sec[name]
         assert s["n_gpus"] == 1 and s["batch"] == n and s["value"] > 0
         assert 0 < s["roofline"]["frac"] < 1
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_line_the_driver_parses():
+    """bench.py's N>1 line end to end at world size 2 (torch.distributed.run,
+    both ranks on this box's GPU, the collectives over gloo on host copies):
+    one JSON line from rank 0 with n_gpus 2, disjoint per-rank game ids,
+    every game of both ranks counted once, and the reduced env-steps and
+    win/loss/draw counts equal to one process playing the same global ids."""
+    import socket
+
+    import torch
+
+    from subproc_amd import ops
+    from subproc_amd.dist import bench_game_id0
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    steps, warmup, games = 3, 1, 65536
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", str(steps), "--warmup", str(warmup), "--games", str(games), "--prewarm-ms", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert REQUIRED <= set(out)
+    cfg = out["config"]
+    assert out["n_gpus"] == 2 and cfg["world_size"] == 2 and cfg["parallelism"] == "dp2"
+    assert cfg["workload"].startswith("config4") and out["scaling"] == "weak"
+    assert cfg["games_counted"] == steps * 2 * games and cfg["global_batch"] == 2 * games
+    per = cfg["game_ids"]["per_rank"]
+    spans = sorted(tuple(x) for rr in per.values() for x in rr)
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))  # disjoint id ranges
+    assert per["0"][0] == [bench_game_id0(warmup, 0, 2, games), bench_game_id0(warmup, 0, 2, games) + games]
+    assert per["1"][0] == [bench_game_id0(warmup, 1, 2, games), bench_game_id0(warmup, 1, 2, games) + games]
+    # the same global ids in one process
+    hist = torch.zeros(133, dtype=torch.int64, device="cuda")
+    for s_ in range(warmup, warmup + steps):
+        for rank in range(2):
+            ops.rollout(games, 0x5EED, bench_game_id0(s_, rank, 2, games), hist=hist, device="cuda",
+                        want_boards=False, want_diff=False, want_plies=False)
+    h = hist.cpu().tolist()
+    assert cfg["env_steps"] == h[132] and cfg["black_white_draw"] == h[129:132]
+    sec = out["secondary"]
+    assert set(sec) == {"step_steady_16M", "step_65536"}
+    for name in sec:
+        assert sec[name]["n_gpus"] == 2 and sec[name]["value"] > 0

@@ -34,7 +34,7 @@ def test_books_match_reference_recorder():
         flat = b.flat_file_bytes(g, "A", "B").decode()
         assert flat == "% Black: A\n% White: B\n" + "".join(line + "\n" for line in bk["lines"])
         for side, col in ((1, 0), (2, 1)):
-            f = b.features(side)[g, :len(bk["lines"])].cpu().numpy()
+            f = b.features(side)[b.game_rows(g)].cpu().numpy()
             assert f.tolist() == [c[col] for c in bk["counts"]], (bk["game"], side)
 
 
@@ -45,15 +45,17 @@ def test_replay_and_text_at_scale_vs_oracle(tmp_path):
     o = oracle.replay(r.moves.cpu().numpy(), r.plies.cpu().numpy())
     pl = r.plies.cpu().numpy()
     gpu_b = U(gb.pos.boards)
+    off = gb.pos.row_off.cpu().numpy()
     for g in range(0, n, 97):
         k = int(pl[g]) + 1
-        np.testing.assert_array_equal(gpu_b[g, :k], o["boards"][g, :k])
-        np.testing.assert_array_equal(gb.pos.turn[g, :k].cpu().numpy(), o["turn"][g, :k])
-        np.testing.assert_array_equal(gb.pos.end[g, :k].cpu().numpy(), o["end"][g, :k])
+        rows = gb.game_rows(g)
+        np.testing.assert_array_equal(gpu_b[rows], o["boards"][g, :k])
+        np.testing.assert_array_equal(gb.pos.turn[rows].cpu().numpy(), o["turn"][g, :k])
+        np.testing.assert_array_equal(gb.pos.end[rows].cpu().numpy(), o["end"][g, :k])
         assert gb.lines(g) == [oracle.serialize_str(b, w, t) for (b, w), t in zip(o["boards"][g, :k], o["turn"][g, :k])]
-        assert gb.pos.end[g, k - 1].item() == 1 and gb.pos.end[g, :k - 1].sum().item() == 0
+        assert int(gb.pos.end[rows][-1]) == 1 and int(gb.pos.end[rows][:-1].sum()) == 0
     # final replayed position == rollout final board
-    last = gpu_b[np.arange(n), pl.astype(np.int64)]
+    last = gpu_b[off + pl.astype(np.int64)]
     np.testing.assert_array_equal(last, U(r.final_boards))
     paths = gb.write_flat_files(str(tmp_path), "t", games=[0, 1])
     assert open(paths[1], "rb").read() == gb.flat_file_bytes(1, "gpu_black", "gpu_white")
@@ -144,3 +146,62 @@ def test_replay_full_size_properties():
     np.testing.assert_array_equal(U(pos.boards[idx].reshape(-1, 2)).reshape(len(idx), 129, 2), o["boards"])
     np.testing.assert_array_equal(pos.turn[idx].cpu().numpy(), o["turn"])
     np.testing.assert_array_equal(pos.end[idx].cpu().numpy(), o["end"])
+
+
+def test_replay_rows_equals_the_strided_table():
+    """oth_replay_rows writes each game's rows 0..plies at row_off[g]: the same
+    rows as oth_replay's stride, from the opening and from mid-game starts
+    (random policy and greedy, whose game lengths differ), 262,144 games."""
+    for n, kw in ((1 << 18, {}), (4096, {"policy": "greedy"})):
+        r = ops.rollout(n, 5, 1 << 33, record_moves=True, device="cuda", **kw)
+        full = ops.replay(r.moves, r.plies)
+        pk = ops.replay_rows(r.moves, r.plies)
+        pl = r.plies.long()
+        inside = torch.arange(129, device="cuda")[None, :] <= pl[:, None]
+        assert pk.boards.shape[0] == int(inside.sum())
+        assert torch.equal(pk.boards, full.boards[inside])
+        assert torch.equal(pk.turn, full.turn[inside]) and torch.equal(pk.end, full.end[inside])
+    z, st, stt = _src("rollout_random_from_mid")
+    mv, plz = torch.as_tensor(z["moves"]).cuda(), torch.as_tensor(z["plies"]).cuda()
+    full = ops.replay(mv, plz, st, stt)
+    pk = ops.replay_rows(mv, plz, st, stt)
+    inside = torch.arange(129, device="cuda")[None, :] <= plz.long()[:, None]
+    assert torch.equal(pk.boards, full.boards[inside]) and torch.equal(pk.turn, full.turn[inside])
+    assert torch.equal(pk.end, full.end[inside])
+
+
+def test_replay_rows_odd_offsets_and_outputs():
+    """Row offsets that are not the prefix sum (a gap after every game, so a
+    block's turn/end range overruns its LDS stage and it stores them directly),
+    outputs at +1 byte (not 16-B aligned), and start turns 0 and 200 (the
+    staged escape): every game's rows equal the strided table's, and the
+    bytes between games are left as they were."""
+    from subproc_amd import _lib
+    n = 700
+    r = ops.rollout(n, 3, 0, record_moves=True, device="cuda")
+    rng = np.random.default_rng(4)
+    start = r.final_boards.clone()
+    stt = torch.as_tensor(rng.choice([0, 1, 2, 200], n).astype(np.uint8)).cuda()
+    mv = torch.as_tensor(rng.integers(0, 66, (n, 128)).astype(np.uint8)).cuda()
+    mv[:, 0] = 64  # a pass first: the start turn row, then put_s turns
+    pl = torch.as_tensor(rng.integers(0, 129, n).astype(np.uint8)).cuda()
+    full = ops.replay(mv, pl, start, stt)
+    inside = torch.arange(129, device="cuda")[None, :] <= pl.long()[:, None]
+    L = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    for gap in (0, 200):
+        cnt = pl.long() + 1 + gap
+        off = (torch.cumsum(cnt, 0) - cnt).contiguous()
+        total = int(cnt.sum())
+        b = torch.full((total + 1, 2), 7, dtype=torch.int64, device="cuda")
+        t = torch.full((total + 17,), 0xAB, dtype=torch.uint8, device="cuda")
+        e = torch.full((total + 17,), 0xCD, dtype=torch.uint8, device="cuda")
+        assert L.oth_replay_rows(start.data_ptr(), stt.data_ptr(), mv.data_ptr(), pl.data_ptr(), off.data_ptr(),
+                                 b.data_ptr(), t.data_ptr() + 1, e.data_ptr() + 1, n, s) == 0
+        rows = (off[:, None] + torch.arange(129, device="cuda")[None, :])[inside]
+        assert torch.equal(b[rows], full.boards[inside]), gap
+        assert torch.equal(t[1:][rows], full.turn[inside]) and torch.equal(e[1:][rows], full.end[inside]), gap
+        untouched = torch.ones(total, dtype=torch.bool, device="cuda")
+        untouched[rows] = False
+        assert bool((t[1:1 + total][untouched] == 0xAB).all()) and bool((e[1:1 + total][untouched] == 0xCD).all())
+        assert int(t[0]) == 0xAB and bool((t[1 + total:] == 0xAB).all())

@@ -44,13 +44,30 @@ class Player:  # game_runner.py:9-64 protocol
         a = re.findall(r"(.+) play ([a-zA-Z][0-9]|PS|ps)", out.rstrip())
         return a[0][1]
 
+    def show_hamlet_param(self):  # game_runner.py:66-73: 'verbose 0' is sent and never read
+        self._w("verbose p\n")
+        b = self.proc.stdout.readline().rstrip()
+        self._w("verbose 0\n")
+        return b
+
+    def show(self):  # game_runner.py:75-102
+        self._w("verbose 1\n")
+        output = "".join(self.proc.stdout.readline() for _ in range(13))
+        b = re.findall(r".*(Black|White|black|white) won.*", output.rstrip())
+        self._w("verbose 0\n")
+        a = re.findall(r".*(Game Over).*", self.proc.stdout.readline().rstrip())
+        won = "None"
+        if len(b) and len(b[0]):
+            won = b[0]
+        return len(a) > 0, won
+
     def end_process(self):
         self._w("quit\n")
         self.proc.stdout.readline()
         self.proc.communicate(timeout=60)
 
 
-def play_a_game(black, white):  # game_runner.py:154-201 without randomisation
+def play_a_game(black, white, end=True):  # game_runner.py:154-201 without randomisation
     black.init()
     white.init()
     b = gboard.Board()
@@ -66,8 +83,9 @@ def play_a_game(black, white):  # game_runner.py:154-201 without randomisation
         dfn.play(ha)
         over = b.is_game_over()
         atk, dfn = dfn, atk
-    black.end_process()
-    white.end_process()
+    if end:
+        black.end_process()
+        white.end_process()
     return b, moves, record
 
 
@@ -145,3 +163,29 @@ def test_engine_greedy_choice_equals_kernel_policy():
         eng.board._set_bits(int(bits[i, 0]), int(bits[i, 1]))
         eng.board.turn = int(pos.turn[i])
         assert codec.move_code(eng.choose().lower()) == first[i], i
+
+
+def test_engine_show_reports_the_winner():
+    """Player.show() (game_runner.py:75-102) on the shim: (False, 'None')
+    mid-game, (True, winner) once the game is over, where the winner is
+    'Black' / 'White' by the final discs ('None' for a draw); the unread
+    'verbose 0' of show_hamlet_param does not desync the protocol."""
+    black = Player(["--policy", "greedy", "--name", "GPU-b", "--seed", "4"])
+    white = Player(["--policy", "random", "--name", "GPU-w", "--seed", "5"])
+    try:
+        assert black.show_hamlet_param() == "GPU-b policy=greedy"
+        black.init()
+        assert black.show() == (False, "None")
+        final, moves, record = play_a_game(black, white, end=False)
+        nb, nw = final.n_black(), final.n_white()
+        want = "Black" if nb > nw else ("White" if nw > nb else "None")
+        assert black.show() == (True, want)
+        assert white.show() == (True, want)
+        assert "policy=random" in white.show_hamlet_param()
+        assert white.show() == (True, want)
+        black.end_process()
+        white.end_process()
+    finally:
+        for p in (black, white):
+            if p.proc.poll() is None:
+                p.proc.kill()

@@ -564,6 +564,39 @@ def test_rollout_captured_in_a_graph_replays_correctly():
         assert torch.equal(mid.hist, ref.hist), k
 
 
+def test_ops_rollout_graphs_replayed_concurrently():
+    """ops.rollout under capture needs its own work word (a replay runs on the
+    replaying stream, so two graphs that baked in one word would share a
+    counter when replayed side by side); with one word per captured launch,
+    two graphs replayed concurrently on two streams both play all their games."""
+    n = 5000
+    want = [ops.rollout(n, 11, k * n, device=DEV) for k in range(2)]
+    words = [torch.zeros(1, dtype=torch.int64, device=DEV) for _ in range(2)]
+    hists = [torch.zeros(133, dtype=torch.int64, device=DEV) for _ in range(2)]
+    graphs, outs = [], []
+    torch.cuda.synchronize()
+    for k in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            with pytest.raises(RuntimeError, match="explicit work word"):
+                ops.rollout(n, 11, k * n, device=DEV)
+            outs.append(ops.rollout(n, 11, k * n, hist=hists[k], device=DEV, work=words[k]))
+        graphs.append(g)
+    streams = [torch.cuda.Stream(DEV) for _ in range(2)]
+    for rep in range(4):
+        for h in hists:
+            h.zero_()
+        torch.cuda.synchronize()
+        for g, st in zip(graphs, streams):
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert torch.equal(outs[k].final_boards, want[k].final_boards), (rep, k)
+            assert torch.equal(hists[k], want[k].hist), (rep, k)
+            assert int(words[k].item()) == 0
+
+
 def _high_mobility_boards(m, seed, iters=400):
     """Hill-climb random boards (single-square mutations kept when Black's
     mobility does not drop) to positions with 24..33 legal moves."""

@@ -27,6 +27,15 @@ def test_state_map_matches_reference_fixture_and_batches_compose():
     for lo, hi in ((0, 1), (1, 100), (100, 256)):
         sm2.update(pos.boards[lo:hi].contiguous(), plies[lo:hi].contiguous())
     assert sm2.items() == want
+    # the packed-rows replay (oth_replay_rows + oth_td_updates_rows), and via GameBooks
+    sm3 = td.StateMap(DEV)
+    pk = ops.replay_rows(moves, plies)
+    assert sm3.update(pk.boards, plies, pk.row_off) == int(2 * (z["plies"].astype(np.int64) + 1).sum())
+    assert sm3.items() == want
+    from subproc_amd.books import GameBooks
+    sm4 = td.StateMap(DEV)
+    sm4.update_from_books(GameBooks(moves, plies))
+    assert sm4.items() == want
     k = next(iter(want))
     assert sm.get(tuple(int(x) for x in k.split(":"))) == want[k]
     assert sm.get((64, 0, 0, 0, 0, 0, 0, 0, 0, 0)) == 0.0

@@ -141,3 +141,23 @@ def test_books_and_features_vs_reference():
             for side, ref in ((1, bk["counts"][k][0]), (2, bk["counts"][k][1])):
                 f = oracle.features(np.array([[bl, wh]], np.uint64), [side])[0]
                 assert list(f) == ref, (bk["game"], k, side)
+
+
+@pytest.mark.parametrize("name", ["rollout_runner_eval", "rollout_runner_greedy", "rollout_runner_eval_mid"])
+def test_runner_schedule_fixtures(name):
+    """GameRunner matches (colour draw, go_for's random-move coin per player)
+    as gen_golden.py drives them through board.py: every move, final board,
+    ply count and colour assignment."""
+    z = load_npz(name + ".npz")
+    n = len(z["plies"])
+    o = oracle.rollout_runner(n, int(z["seed"]), int(z["game_id0"]), int(z["policy"]), z["weights_a"],
+                              z["weights_b"], int(z["n_rand_a"]), int(z["n_rand_b"]), bool(z["swap"]),
+                              start=np.stack([z["start_black"], z["start_white"]], 1), start_turn=z["start_turn"],
+                              record_moves=True)
+    np.testing.assert_array_equal(o["moves"], z["moves"])
+    np.testing.assert_array_equal(o["final_boards"], np.stack([z["final_black"], z["final_white"]], 1))
+    np.testing.assert_array_equal(o["plies"], z["plies"])
+    np.testing.assert_array_equal(o["diff"], z["diff"])
+    np.testing.assert_array_equal(o["a_black"], z["a_black"])
+    if bool(z["swap"]):
+        assert 0 < int(z["a_black"].sum()) < n  # both colour assignments occur

@@ -148,6 +148,13 @@ struct Position {
     u64 legal;  // Board.puttables as a mask (board.py:46-52) = reach & empty
 };
 
+// ORDER: the order the six Kogge-Stone fills are written in (digits = the
+// direction pairs 7/8/9).  It only steers hipcc's register allocation: a
+// v_bitop3_b32 whose three sources sit in one VGPR bank issues in 4.3 cycles
+// instead of 2.5, and the bit pairs of 64-bit values make that likely; the
+// order with the fewest such instructions in each kernel's hot loop was picked
+// by tools/valu_mix.py (random rollout: 7-9-8, 11 -> 3 per ply).
+template <int ORDER = 798>
 __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     const u64 Oi = O & INNER_FILES;
     s.Oi = Oi;
@@ -161,12 +168,22 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     // west (-1): the same on the bit-reversed board
     s.A[1] = rev64(east_run(rev64(P), s.rOi));
     // the Kogge-Stone fills from P stay inside P | O, so "minus P" is "and O"
-    s.A[2] = ks<8, true>(P, v) & O;
-    s.A[3] = ks<8, false>(P, v) & O;
-    s.A[4] = ks<9, true>(P, d9) & O;
-    s.A[5] = ks<9, false>(P, d9) & O;
-    s.A[6] = ks<7, true>(P, d7) & O;
-    s.A[7] = ks<7, false>(P, d7) & O;
+    {
+        constexpr int order[3] = {ORDER / 100, ORDER / 10 % 10, ORDER % 10};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (order[k] == 8) {
+                s.A[2] = ks<8, true>(P, v) & O;
+                s.A[3] = ks<8, false>(P, v) & O;
+            } else if (order[k] == 9) {
+                s.A[4] = ks<9, true>(P, d9) & O;
+                s.A[5] = ks<9, false>(P, d9) & O;
+            } else {
+                s.A[6] = ks<7, true>(P, d7) & O;
+                s.A[7] = ks<7, false>(P, d7) & O;
+            }
+        }
+    }
     // a legal square is one step beyond an attached run, and empty
     u64 m = or3(sh<1, true>(s.A[0]), sh<1, false>(s.A[1]), sh<8, true>(s.A[2]));
     m = or3(m, sh<8, false>(s.A[3]), sh<9, true>(s.A[4]));
@@ -349,9 +366,10 @@ __device__ __forceinline__ u64 flips_runs(u32 sq, const RunSets& r) {
 }
 
 // legal moves only (no run sets kept) — for child positions / next-state masks
+template <int ORDER = 798>
 __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;
-    analyse(P, O, s);
+    analyse<ORDER>(P, O, s);
     return s.legal;
 }
 

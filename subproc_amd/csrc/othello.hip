@@ -73,11 +73,7 @@ __device__ __forceinline__ u32 pick_legal(u64 legal, GameRng& rng, const uint8_t
     const u32 c_lo = __popc((u32)legal);
     return kth_bit_tab(legal, rng.pick(c_lo + __popc((u32)(legal >> 32))), c_lo, kth_tab);
 }
-// the same pick as 8 x the square (the byte offset into the LDS ray table)
-__device__ __forceinline__ u32 pick_legal_off(u64 legal, GameRng& rng, const uint8_t* kth_tab) {
-    const u32 c_lo = __popc((u32)legal);
-    return kth_bit_off(legal, rng.pick(c_lo + __popc((u32)(legal >> 32))), c_lo, kth_tab);
-}
+
 
 // counts() region masks a..h (parameter_progress_position_moves_learn.py:9-16)
 __constant__ u64 kRegionMasks[8] = {0x8100000000000081ull, 0x4281000000008142ull, 0x0042000000004200ull,
@@ -123,7 +119,7 @@ __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq,
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
-    const int v = eval_linear(w, P2, moves(P2, O2));  // |v| < 2^14
+    const int v = eval_linear(w, P2, moves<879>(P2, O2));  // |v| < 2^14 (fill order: bitboard.hpp analyse)
     return ((u32)((1 << 20) - v) << 6) | sq;
 }
 
@@ -578,15 +574,21 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
             const bool b0 = side == OTH_BLACK;
             const u32 discs0 = RECORD ? 0u : (u32)__popcll(P | O);
             u32 npass = 0;  // passes (RECORD: every ply)
-            // one ply of mover X against Y (X black iff x_black); true at the terminal
-            auto ply_of = [&](u64& X, u64& Y, const bool x_black) -> bool {
+            // one ply of mover X against Y; true at the terminal.  The
+            // terminal's bookkeeping (final board, diff, plies, histogram) is
+            // done once per lane after the loop, where P is still side0's
+            // discs: inside it, the block ran whenever any lane of the wave
+            // ended, ~7 times per batch.
+            auto ply_of = [&](u64& X, u64& Y) -> bool {
 #ifdef OTH_DIAG
                 diag_iters++;
 #endif
                 Position pos;
                 analyse(X, Y, pos);
                 const u64 legal = pos.legal;
-                if (legal == 0) {
+                // the move count serves the zero test and the pick
+                const u32 c_lo = __popc((u32)legal), nl = c_lo + __popc((u32)(legal >> 32));
+                if (nl == 0) {
                     // a full board is terminal at once: the other side has no
                     // empty square either, so the hand-over iteration (a
                     // second analysis) is skipped; 65% of random games end so
@@ -594,17 +596,6 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         // terminal: both sides without a legal move (board.py:57-58);
                         // a pass handed over just before is not an env-step
                         if (passed) npass--;
-                        const u32 ply = RECORD ? npass : (u32)__popcll(X | Y) - discs0 + npass;
-                        if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
-                        const u64 bl = x_black ? X : Y, wh = x_black ? Y : X;
-                        const int d = __popcll(bl) - __popcll(wh);
-                        if (a.final_boards)
-                            reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
-                        if (a.diff) a.diff[g] = (int8_t)d;
-                        if (a.plies) a.plies[g] = (uint8_t)ply;
-                        atomicAdd(&hist_s[d + 64], 1ull);
-                        atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
-                        plies_sum += ply;
                         return true;
                     }
                     // the mover must pass ('PS'): hand the move over
@@ -614,7 +605,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     return false;
                 }
                 passed = false;
-                const u32 off = pick_legal_off(legal, rng, kth_tab);
+                const u32 off = kth_bit_off(legal, rng.pick(nl), c_lo, kth_tab);
                 const u64* col = ray_col(rays, off);
                 const Flips f = flips_col(col[kRayRows * 64], run_sets(pos), col);
                 if (RECORD) {
@@ -626,9 +617,19 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
             };
             if (active) {
                 for (;;) {
-                    if (ply_of(P, O, b0)) break;
-                    if (ply_of(O, P, !b0)) break;
+                    if (ply_of(P, O)) break;
+                    if (ply_of(O, P)) break;
                 }
+                const u32 ply = RECORD ? npass : (u32)__popcll(P | O) - discs0 + npass;
+                if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
+                const u64 bl = b0 ? P : O, wh = b0 ? O : P;
+                const int d = __popcll(bl) - __popcll(wh);
+                if (a.final_boards) reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
+                if (a.diff) a.diff[g] = (int8_t)d;
+                if (a.plies) a.plies[g] = (uint8_t)ply;
+                atomicAdd(&hist_s[d + 64], 1ull);
+                atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
+                plies_sum += ply;
             }
         } else {
             // GameRunner schedule (RUNNER): the colour draw, then the random

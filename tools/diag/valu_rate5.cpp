@@ -69,6 +69,29 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed) {
                                          "v_and_b32 v61, v49, v50", "v_and_b32 v62, v53, v54")) ::: CLOB);
         if (OP == 22) asm volatile(X8(R4("v_mov_b32 v56, v41", "v_mov_b32 v58, v45", "v_mov_b32 v60, v49", "v_mov_b32 v62, v53")) ::: CLOB);
         if (OP == 23) asm volatile(X8(R4("v_or_b32 v56, v41, v42", "v_xor_b32 v58, v45, v46", "v_or_b32 v60, v49, v50", "v_xor_b32 v62, v53, v54")) ::: CLOB);
+        // round 3: other candidate classes (sub-dword selects, funnel/byte shifts, 24-bit multiplies, fused 3-op)
+        if (OP == 24) asm volatile(X8(R4("v_mov_b32_sdwa v56, v41 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0", "v_mov_b32_sdwa v58, v45 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0",
+                                         "v_mov_b32_sdwa v60, v49 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0", "v_mov_b32_sdwa v62, v53 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0")) ::: CLOB);
+        if (OP == 25) asm volatile(X8(R4("v_and_b32_sdwa v56, v41, v42 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD", "v_and_b32_sdwa v58, v45, v46 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD",
+                                         "v_and_b32_sdwa v60, v49, v50 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD", "v_and_b32_sdwa v62, v53, v54 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD")) ::: CLOB);
+        if (OP == 26) asm volatile(X8(R4("v_alignbit_b32 v56, v41, v42, 8", "v_alignbit_b32 v58, v45, v46, 8", "v_alignbit_b32 v60, v49, v50, 8", "v_alignbit_b32 v62, v53, v54, 8")) ::: CLOB);
+        if (OP == 27) asm volatile(X8(R4("v_alignbyte_b32 v56, v41, v42, 1", "v_alignbyte_b32 v58, v45, v46, 1", "v_alignbyte_b32 v60, v49, v50, 1", "v_alignbyte_b32 v62, v53, v54, 1")) ::: CLOB);
+        if (OP == 28) asm volatile(X8(R4("v_perm_b32 v56, v41, v42, v43", "v_perm_b32 v58, v45, v46, v47", "v_perm_b32 v60, v49, v50, v51", "v_perm_b32 v62, v53, v54, v55")) ::: CLOB);
+        if (OP == 29) asm volatile(X8(R4("v_mul_u32_u24 v56, v41, v42", "v_mul_u32_u24 v58, v45, v46", "v_mul_u32_u24 v60, v49, v50", "v_mul_u32_u24 v62, v53, v54")) ::: CLOB);
+        if (OP == 30) asm volatile(X8(R4("v_mad_u32_u24 v56, v41, v42, v43", "v_mad_u32_u24 v58, v45, v46, v47", "v_mad_u32_u24 v60, v49, v50, v51", "v_mad_u32_u24 v62, v53, v54, v55")) ::: CLOB);
+        if (OP == 31) asm volatile(X8(R4("v_lshl_or_b32 v56, v41, 8, v42", "v_lshl_or_b32 v58, v45, 8, v46", "v_lshl_or_b32 v60, v49, 8, v50", "v_lshl_or_b32 v62, v53, 8, v54")) ::: CLOB);
+        if (OP == 32) asm volatile(X8(R4("v_add_u32 v56, v41, v42", "v_add_u32 v58, v45, v46", "v_add_u32 v60, v49, v50", "v_add_u32 v62, v53, v54")) ::: CLOB);
+        if (OP == 33) asm volatile(X8(R4("v_pk_mov_b32 v[56:57], v[42:43], v[42:43] op_sel:[0,1]", "v_pk_mov_b32 v[58:59], v[46:47], v[46:47] op_sel:[0,1]",
+                                         "v_pk_mov_b32 v[60:61], v[50:51], v[50:51] op_sel:[0,1]", "v_pk_mov_b32 v[62:63], v[54:55], v[54:55] op_sel:[0,1]")) ::: CLOB);
+        if (OP == 34) asm volatile(X8(R4("v_pk_lshlrev_b16 v56, 8, v42", "v_pk_lshlrev_b16 v58, 8, v46", "v_pk_lshlrev_b16 v60, 8, v50", "v_pk_lshlrev_b16 v62, 8, v54")) ::: CLOB);
+        if (OP == 35) asm volatile(X8(R4("v_lshlrev_b16 v56, 8, v42", "v_lshlrev_b16 v58, 8, v46", "v_lshlrev_b16 v60, 8, v50", "v_lshlrev_b16 v62, 8, v54")) ::: CLOB);
+        if (OP == 36) asm volatile(X8(R4("v_ffbh_u32 v56, v42", "v_ffbh_u32 v58, v46", "v_ffbh_u32 v60, v50", "v_ffbh_u32 v62, v54")) ::: CLOB);
+        if (OP == 37) asm volatile(X8(R4("v_bitop3_b16 v56, v41, v42, v43 bitop3:0xca", "v_bitop3_b16 v60, v45, v46, v47 bitop3:0xca",
+                                         "v_bitop3_b16 v56, v49, v50, v51 bitop3:0xca", "v_bitop3_b16 v60, v53, v54, v55 bitop3:0xca")) ::: CLOB);
+        if (OP == 38) asm volatile(X8(R4("v_mov_b64 v[56:57], v[42:43]", "v_mov_b64 v[58:59], v[46:47]", "v_mov_b64 v[60:61], v[50:51]", "v_mov_b64 v[62:63], v[54:55]")) ::: CLOB);
+        if (OP == 39) asm volatile(X8(R4("v_not_b32 v56, v42", "v_not_b32 v58, v46", "v_not_b32 v60, v50", "v_not_b32 v62, v54")) ::: CLOB);
+        if (OP == 40) asm volatile(X8(R4("v_and_or_b32 v56, v41, v42, v43", "v_and_or_b32 v58, v45, v46, v47", "v_and_or_b32 v60, v49, v50, v51", "v_and_or_b32 v62, v53, v54, v55")) ::: CLOB);
+        if (OP == 41) asm volatile(X8(R4("v_mbcnt_lo_u32_b32 v56, v42, 0", "v_mbcnt_lo_u32_b32 v58, v46, 0", "v_mbcnt_lo_u32_b32 v60, v50, 0", "v_mbcnt_lo_u32_b32 v62, v54, 0")) ::: CLOB);
     }
     unsigned r;
     asm volatile("v_mov_b32 %0, v56" : "=v"(r)::CLOB);
@@ -126,5 +149,23 @@ int main() {
     report<21>(out, "1 lshlrev_b64 + 3 and_b32 (per instr)", b);
     report<22>(out, "mov_b32", b);
     report<23>(out, "or / xor", b);
+    report<24>(out, "mov_b32_sdwa (x << 16 as a word move)", b);
+    report<25>(out, "and_b32_sdwa (byte 1 of src0)", b);
+    report<26>(out, "alignbit_b32 (funnel shift 8)", b);
+    report<27>(out, "alignbyte_b32 (funnel shift 1 byte)", b);
+    report<28>(out, "perm_b32", b);
+    report<29>(out, "mul_u32_u24", b);
+    report<30>(out, "mad_u32_u24", b);
+    report<31>(out, "lshl_or_b32", b);
+    report<32>(out, "add_u32", b);
+    report<33>(out, "pk_mov_b32 (64-bit swap halves)", b);
+    report<34>(out, "pk_lshlrev_b16", b);
+    report<35>(out, "lshlrev_b16", b);
+    report<36>(out, "ffbh_u32", b);
+    report<37>(out, "bitop3_b16", b);
+    report<38>(out, "mov_b64", b);
+    report<39>(out, "not_b32", b);
+    report<40>(out, "and_or_b32", b);
+    report<41>(out, "mbcnt_lo_u32_b32", b);
     return 0;
 }

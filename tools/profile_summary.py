@@ -24,10 +24,19 @@ N_SIMD = 1024
 
 
 def short(name):
-    for k in ("rollout_kernel<0, false>", "rollout_kernel<1, false>", "rollout_kernel<2, false>",
-              "rollout_kernel<0, true>", "rollout_kernel<1, true>", "rollout_kernel<2, true>", "step_kernel",
-              "legal_kernel", "result_kernel", "reset_kernel", "sample_midgame_kernel", "replay_kernel",
-              "book_text_kernel", "features_kernel", "eval_kernel", "td_updates_kernel", "td_ema_kernel"):
+    """Stable short names: rollout_kernel<POLICY, RECORD> (the GameRunner
+    instances as rollout_runner<POLICY, RECORD>), replay_kernel (strided) and
+    replay_rows_kernel (packed rows, round 3)."""
+    import re
+    m = re.search(r"rollout_kernel<(\d), (true|false)(?:, (true|false))?>", name)
+    if m:
+        return "rollout_%s<%s, %s>" % ("runner" if m.group(3) == "true" else "kernel", m.group(1), m.group(2))
+    m = re.search(r"replay_kernel<(true|false)>", name)
+    if m:
+        return "replay_rows_kernel" if m.group(1) == "true" else "replay_kernel"
+    for k in ("step_kernel", "legal_kernel", "result_kernel", "reset_kernel", "sample_midgame_kernel",
+              "replay_kernel", "book_text_kernel", "features_kernel", "eval_kernel", "td_updates_kernel",
+              "td_ema_kernel"):
         if k in name:
             return k
     return None

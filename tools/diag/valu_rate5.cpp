@@ -91,6 +91,22 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed) {
         if (OP == 38) asm volatile(X8(R4("v_mov_b64 v[56:57], v[42:43]", "v_mov_b64 v[58:59], v[46:47]", "v_mov_b64 v[60:61], v[50:51]", "v_mov_b64 v[62:63], v[54:55]")) ::: CLOB);
         if (OP == 39) asm volatile(X8(R4("v_not_b32 v56, v42", "v_not_b32 v58, v46", "v_not_b32 v60, v50", "v_not_b32 v62, v54")) ::: CLOB);
         if (OP == 40) asm volatile(X8(R4("v_and_or_b32 v56, v41, v42, v43", "v_and_or_b32 v58, v45, v46, v47", "v_and_or_b32 v60, v49, v50, v51", "v_and_or_b32 v62, v53, v54, v55")) ::: CLOB);
+        if (OP == 42) asm volatile(X8(R4("v_sub_u32 v56, v41, v42", "v_sub_u32 v58, v45, v46", "v_sub_u32 v60, v49, v50", "v_sub_u32 v62, v53, v54")) ::: CLOB);
+        if (OP == 43) asm volatile(X8(R4("v_min_u32 v56, v41, v42", "v_min_u32 v58, v45, v46", "v_min_u32 v60, v49, v50", "v_min_u32 v62, v53, v54")) ::: CLOB);
+        if (OP == 44) asm volatile(X8(R4("v_add_co_u32 v56, vcc, v41, v42", "v_add_co_u32 v58, vcc, v45, v46", "v_add_co_u32 v60, vcc, v49, v50", "v_add_co_u32 v62, vcc, v53, v54")) ::: CLOB);
+        if (OP == 45) asm volatile(X8(R4("v_addc_co_u32 v56, vcc, v41, v42, vcc", "v_addc_co_u32 v58, vcc, v45, v46, vcc", "v_addc_co_u32 v60, vcc, v49, v50, vcc", "v_addc_co_u32 v62, vcc, v53, v54, vcc")) ::: CLOB);
+        if (OP == 46) asm volatile(X8(R4("v_lshrrev_b16 v56, 8, v42", "v_lshrrev_b16 v58, 8, v46", "v_lshrrev_b16 v60, 8, v50", "v_lshrrev_b16 v62, 8, v54")) ::: CLOB);
+        if (OP == 47) asm volatile(X8(R4("v_lshlrev_b16_sdwa v56, 8, v42 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:WORD_1", "v_lshlrev_b16_sdwa v58, 8, v46 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:WORD_1", "v_lshlrev_b16_sdwa v60, 8, v50 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:WORD_1", "v_lshlrev_b16_sdwa v62, 8, v54 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:WORD_1")) ::: CLOB);
+        if (OP == 48) asm volatile(X8(R4("v_add_u16 v56, v41, v42", "v_add_u16 v58, v45, v46", "v_add_u16 v60, v49, v50", "v_add_u16 v62, v53, v54")) ::: CLOB);
+        if (OP == 49) asm volatile(X8(R4("v_max_u32 v56, v41, v42", "v_max_u32 v58, v45, v46", "v_max_u32 v60, v49, v50", "v_max_u32 v62, v53, v54")) ::: CLOB);
+        if (OP == 50) asm volatile(X8(R4("v_add3_u32 v56, v41, v42, v43", "v_add3_u32 v58, v45, v46, v47", "v_add3_u32 v60, v49, v50, v51", "v_add3_u32 v62, v53, v54, v55")) ::: CLOB);
+        if (OP == 51) asm volatile(X8(R4("v_cmp_gt_u32_e32 vcc, v41, v42", "v_cmp_gt_u32_e32 vcc, v45, v46", "v_cmp_gt_u32_e32 vcc, v49, v50", "v_cmp_gt_u32_e32 vcc, v53, v54")) ::: CLOB);
+        if (OP == 52) asm volatile(X8(R4("v_and_b32 v56, 0x7e7e7e7e, v42", "v_and_b32 v58, 0x7e7e7e7e, v46", "v_and_b32 v60, 0x7e7e7e7e, v50", "v_and_b32 v62, 0x7e7e7e7e, v54")) ::: CLOB);
+        if (OP == 53) asm volatile(X8(R4("v_cmp_gt_u32_e32 vcc, v41, v42", "v_cndmask_b32_e32 v58, v45, v46, vcc", "v_cmp_gt_u32_e32 vcc, v49, v50", "v_cndmask_b32_e32 v62, v53, v54, vcc")) ::: CLOB);
+        if (OP == 54) asm volatile(X8(R4("v_mul_lo_u16 v56, v41, v42", "v_mul_lo_u16 v58, v45, v46", "v_mul_lo_u16 v60, v49, v50", "v_mul_lo_u16 v62, v53, v54")) ::: CLOB);
+        if (OP == 55) asm volatile(X8(R4("v_lshlrev_b32_e64 v56, v41, v42", "v_lshlrev_b32_e64 v58, v45, v46", "v_lshlrev_b32_e64 v60, v49, v50", "v_lshlrev_b32_e64 v62, v53, v54")) ::: CLOB);
+        if (OP == 56) asm volatile(X8(R4("v_sub_u16 v56, v41, v42", "v_sub_u16 v58, v45, v46", "v_sub_u16 v60, v49, v50", "v_sub_u16 v62, v53, v54")) ::: CLOB);
+        if (OP == 57) asm volatile(X8(R4("v_min_u16 v56, v41, v42", "v_min_u16 v58, v45, v46", "v_min_u16 v60, v49, v50", "v_min_u16 v62, v53, v54")) ::: CLOB);
         if (OP == 41) asm volatile(X8(R4("v_mbcnt_lo_u32_b32 v56, v42, 0", "v_mbcnt_lo_u32_b32 v58, v46, 0", "v_mbcnt_lo_u32_b32 v60, v50, 0", "v_mbcnt_lo_u32_b32 v62, v54, 0")) ::: CLOB);
     }
     unsigned r;
@@ -167,5 +183,21 @@ int main() {
     report<39>(out, "not_b32", b);
     report<40>(out, "and_or_b32", b);
     report<41>(out, "mbcnt_lo_u32_b32", b);
+    report<42>(out, "sub_u32", b);
+    report<43>(out, "min_u32", b);
+    report<44>(out, "add_co_u32 (carry out)", b);
+    report<45>(out, "addc_co_u32 (carry in and out)", b);
+    report<46>(out, "lshrrev_b16", b);
+    report<47>(out, "lshlrev_b16_sdwa (high word, preserve)", b);
+    report<48>(out, "add_u16", b);
+    report<49>(out, "max_u32", b);
+    report<50>(out, "add3_u32", b);
+    report<51>(out, "cmp_gt_u32_e32 (vcc)", b);
+    report<52>(out, "and_b32 with a literal", b);
+    report<53>(out, "cmp_e32 + cndmask_e32 pair (per instr)", b);
+    report<54>(out, "mul_lo_u16", b);
+    report<55>(out, "lshlrev_b32_e64 (variable)", b);
+    report<56>(out, "sub_u16", b);
+    report<57>(out, "min_u16", b);
     return 0;
 }

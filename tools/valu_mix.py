@@ -25,18 +25,23 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # Measured on the box (tools/diag/valu_rate5.cpp: 32 independent instructions
-# on fixed registers, 8 waves/SIMD): only bitwise logic and moves stream at
-# ~2.2 cycles per wave-instruction; v_bitop3_b32 at 2.5 -- 4.3 when its three
-# source registers are distinct and in one VGPR bank (bank = number mod 4);
-# everything else these kernels use, 32-bit add/sub/min and compares
-# included, at 4.1-4.4.
-FAST = re.compile(r"^v_(and|or|xor|not|mov)_(b32|b64)(_e32)?$")
+# on fixed registers, 8 waves/SIMD): bitwise logic, moves, 32-bit add/sub
+# without carry and the 16-bit VOP2 ops stream at ~2.2 cycles per
+# wave-instruction; v_bitop3_b32 at 2.5 -- 4.3 when its three source registers
+# are distinct and in one VGPR bank (bank = number mod 4); every shift,
+# min/max, compare, carry, select, popcount and 64-bit op at 4.0-4.4.
+FAST = re.compile(r"^v_((and|or|xor|not|mov)_b32|(add|sub)_u32|(lshlrev|lshrrev)_b16|(add|sub|min)_u16|mul_lo_u16)(_e32)?$")
 FAST_CYC, SLOW_CYC = 2.2, 4.2
 BITOP3_CYC, BITOP3_CONFLICT_CYC = 2.5, 4.3
 MEASURED = {"v_lshlrev_b64": 4.25, "v_lshrrev_b64": 4.22, "v_lshl_add_u64": 4.24, "v_bfrev_b32_e32": 4.13,
             "v_lshlrev_b32_e32": 4.07, "v_bcnt_u32_b32": 4.09, "v_mul_hi_u32": 4.29, "v_mad_u64_u32": 4.43,
             "v_cndmask_b32_e64": 4.2, "v_bfe_u32": 4.25, "v_min_u32_e32": 4.08, "v_sub_u32_e32": 4.08,
-            "v_bfi_b32": 4.2, "v_or3_b32": 4.2, "v_alignbit_b32": 4.2, "v_perm_b32": 4.3}
+            "v_bfi_b32": 4.2, "v_or3_b32": 4.2, "v_alignbit_b32": 4.12, "v_perm_b32": 4.2,
+            # round 3 (valu_rate5.cpp OPs 24-57)
+            "v_add_u32_e32": 2.19, "v_sub_u32_e32": 2.24, "v_min_u32_e32": 4.06, "v_max_u32_e32": 4.05,
+            "v_add_co_u32_e32": 4.09, "v_sub_co_u32_e32": 4.09, "v_sub_co_u32_e64": 4.09, "v_addc_co_u32_e32": 4.09,
+            "v_cmp_gt_u32_e32": 4.03, "v_cndmask_b32_e32": 4.0, "v_add3_u32": 4.13, "v_lshl_or_b32": 4.10,
+            "v_and_or_b32": 4.11, "v_mov_b64_e32": 4.14, "v_ffbh_u32_e32": 4.05, "v_bfe_u32": 4.20}
 
 
 def bank_conflict(line):

@@ -303,10 +303,11 @@ def rollout_runner(n, seed, game_id0=0, policy="eval", weights_a=None, weights_b
                                             int(n_rand_b), int(bool(swap_colours)), ab.data_ptr(), fb.data_ptr(),
                                             df.data_ptr(), pl.data_ptr(), None if mv is None else mv.data_ptr(), ph,
                                             pw, n, _stream())
-        if rc != _lib.OTH_OK and work is not None and not torch.cuda.is_current_stream_capturing():
-            w.zero_()
-        elif rc != _lib.OTH_OK:
-            _WORK.pop((d.index, torch.cuda.current_stream().cuda_stream), None)
+        if rc != _lib.OTH_OK:  # as ops.rollout: drop the stream's default word, reset a caller's eagerly
+            if work is None:
+                _WORK.pop((d.index, torch.cuda.current_stream().cuda_stream), None)
+            elif not torch.cuda.is_current_stream_capturing():
+                w.zero_()
         check(rc, "oth_rollout_runner")
     return RunnerResult(fb, df, pl, mv, hist, ab)
 

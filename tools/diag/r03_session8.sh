@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-3 session 8: smoke() and the bench line at the driver's arguments.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/s8
+mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/bench.json').read().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['valu']['frac'], d['roofline']['traffic'])"

@@ -21,7 +21,8 @@ Also reported on rank 0 (secondary, same JSON line):
   * eval       : 1,048,576 games of the 1-ply linear-eval policy with the
     learner's default weights (SURVEY.md §8f row 2);
   * td_state_map: the learner's TD state-map update for 262,144 GPU games;
-  * book_emitter: replay and serialize_str text of 262,144 games (§8f row 1);
+  * book_emitter: replay and serialize_str text of 262,144 games (§8f row 1),
+    and the text parsed back by the reader's kernel (oth_book_parse);
   * cpu_baseline: the C oracle (mailbox restatement of board.py) on a bounded
     sample of the same workload on the host cores.
 
@@ -563,11 +564,31 @@ def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
     us = timed(lambda: ops.book_text(pk.boards, pk.turn))
     tb = rows * (16 + 1 + 67)
     out["book_text"] = {"lines": rows, "us": us, "achieved_gbs": tb / us / 1e3, "frac_hbm": tb / us / 1e3 / HBM_PEAK_GBS}
+    # the reader's side: the same text parsed back in place (oth_book_parse,
+    # stride 67 with the side to move) -- checked against the rows it came from
+    text = ops.book_text(pk.boards, pk.turn)
+    pb, pt = ops.book_parse(text, rows, stride=67, want_turn=True)
+    if not (torch.equal(pb, pk.boards) and torch.equal(pt, pk.turn)):
+        raise SystemExit("bench: oth_book_parse did not give back the replayed rows")
+    us = timed(lambda: ops.book_parse(text, rows, stride=67, want_turn=True))
+    pbytes = rows * (67 + 16 + 1)
+    out["book_parse"] = {"lines": rows, "us": us, "achieved_gbs": pbytes / us / 1e3,
+                         "frac_hbm": pbytes / us / 1e3 / HBM_PEAK_GBS}
+    del text, pb, pt
+    packed = torch.empty(rows * 64, dtype=torch.uint8, device=dev).view(rows, 64)
+    packed.copy_(ops.book_text(pk.boards, pk.turn).view(rows, 67)[:, :64])
+    packed = packed.view(-1)
+    us = timed(lambda: ops.book_parse(packed, rows, stride=64))
+    pbytes = rows * (64 + 16)
+    out["book_parse_packed"] = {"lines": rows, "us": us, "achieved_gbs": pbytes / us / 1e3,
+                                "frac_hbm": pbytes / us / 1e3 / HBM_PEAK_GBS}
+    del packed
     us = timed(lambda: ops.replay(r.moves, r.plies))
     sb = games * (128 + 1 + 129 * 18)  # the strided table: all 129 rows per game written
     out["replay_strided"] = {"games": games, "us": us, "achieved_gbs": sb / us / 1e3,
                              "useful_gbs": rb / us / 1e3, "frac_hbm": sb / us / 1e3 / HBM_PEAK_GBS}
-    out["metric"] = "book emitter (packed replay + serialize_str text) per 262,144 games"
+    out["metric"] = ("book emitter (packed replay + serialize_str text) per 262,144 games; book_parse: the text "
+                     "parsed back (flat-file lines, and packed 64-byte strings)")
     return out
 
 

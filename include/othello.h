@@ -217,6 +217,18 @@ int oth_replay_rows(const uint64_t* start, const uint8_t* start_turn, const uint
  * (game_recorder.py:67-76). */
 int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* out, void* stream);
 
+/* Book ingest, the reader's side of the same format (game_reader.py:60-75 /
+ * replearn.learn_books, replearn.py:27-46): the board strings of n records --
+ * 64 chars at text + i*stride, char k for square (k % 8, k / 8) -- into
+ * boards[i] = {black, white} as Board.deserialize sets them on a fresh Board
+ * (board.py:253-258 with turn_from_string, 245-251: 'O' Black, 'X' White, any
+ * other byte Empty).  stride >= 64: 64 for packed strings, OTH_BOOK_LINE for
+ * the serialize_str lines of a FlatFileRecorder file (game_recorder.py:67-76).
+ * turn (may be NULL; needs stride >= 66) receives turn_from_string of byte 65,
+ * the side after the board's space.  Replaces the per-record
+ * board_from_a_book (parameter.py:5-8) of the learner. */
+int oth_book_parse(const char* text, int64_t stride, uint64_t* boards, uint8_t* turn, int64_t n, void* stream);
+
 /* Learner features: counts() of parameter_progress_position_moves_learn.py:5-17
  * for side[i] in {1 = 'O', 2 = 'X'}: out[i*10 + 0] = 64 - n_empty,
  * [1] = n_puttable_for(side), [2..9] = mask_count(side, region mask a..h). */
@@ -251,6 +263,20 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
  * row_off[g] + p (device, n int64). */
 int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                         const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream);
+
+/* oth_td_updates over book records in the learner's own order
+ * (learn_and_update_batch -> __update_state_for_a_book,
+ * progress_position_moves_learn.py:37-62, 94-96), for books from any source:
+ * row r of rows (record boards, e.g. from oth_book_parse; books concatenated in
+ * batch order, each book's records as given, terminal record first) is update
+ * pair 2r ('O') and 2r + 1 ('X'):
+ *   keys[2r + s]   = OTH_TD_KEY(counts(row r, side s))
+ *   values[2r + s] = (double)value_s(rows[term_row[r]]) * lam_pow[lam_idx[r]]
+ * term_row[r]: the row of r's book's first record (book[0], whose board gives
+ * value_O = n_black - n_white and value_X = -value_O); lam_pow[lam_idx[r]]:
+ * l ** (last_turn - turn) of the record, from the caller's table. */
+int oth_td_updates_records(const uint64_t* rows, const int64_t* term_row, const int32_t* lam_idx,
+                           const double* lam_pow, int64_t* keys, double* values, int64_t n_rows, void* stream);
 
 /* TD state map, step 2: segment s (updates seg_off[s] .. seg_off[s+1]-1 of one
  * key, in stream order) starts from init[s] and applies, in order,

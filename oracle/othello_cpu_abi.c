@@ -183,6 +183,25 @@ int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* 
     return OTH_OK;
 }
 
+/* Board.deserialize of each 64-char string onto a fresh Board, one char at a
+ * time (board.py:253-258): 'O' Black, 'X' White, anything else Empty */
+int oth_book_parse(const char* text, int64_t stride, uint64_t* boards, uint8_t* turn, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || stride < 64 || (turn && stride < 66) || (n > 0 && (!text || !boards))) return OTH_EINVAL;
+    for (int64_t i = 0; i < n; i++) {
+        const char* s = text + i * stride;
+        uint64_t bl = 0, wh = 0;
+        for (int sq = 0; sq < 64; sq++) {
+            if (s[sq] == 'O') bl |= 1ull << sq;
+            else if (s[sq] == 'X') wh |= 1ull << sq;
+        }
+        boards[2 * i] = bl;
+        boards[2 * i + 1] = wh;
+        if (turn) turn[i] = s[65] == 'O' ? OTH_BLACK : (s[65] == 'X' ? OTH_WHITE : 0);
+    }
+    return OTH_OK;
+}
+
 int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream) {
     (void)stream;
     if (n < 0 || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
@@ -232,6 +251,27 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     if (n < 0 || (n > 0 && (!pos_boards || !row_off || !plies || !base || !lam_pow || !keys || !values)))
         return OTH_EINVAL;
     return td_updates_any(pos_boards, row_off, plies, base, lam_pow, keys, values, n);
+}
+
+int oth_td_updates_records(const uint64_t* rows, const int64_t* term_row, const int32_t* lam_idx,
+                           const double* lam_pow, int64_t* keys, double* values, int64_t n_rows, void* stream) {
+    (void)stream;
+    if (n_rows < 0 || (n_rows > 0 && (!rows || !term_row || !lam_idx || !lam_pow || !keys || !values)))
+        return OTH_EINVAL;
+    for (int64_t r = 0; r < n_rows; r++) {
+        int8_t d;
+        oracle_result(rows + 2 * term_row[r], NULL, NULL, &d, NULL, 1);
+        uint8_t f[2][10];
+        const uint8_t sides[2] = {OTH_BLACK, OTH_WHITE};
+        const uint64_t b2[4] = {rows[2 * r], rows[2 * r + 1], rows[2 * r], rows[2 * r + 1]};
+        oracle_features(b2, sides, &f[0][0], 2);
+        const double lam = lam_pow[lam_idx[r]];
+        keys[2 * r] = td_key(f[0]);
+        values[2 * r] = (double)d * lam;
+        keys[2 * r + 1] = td_key(f[1]);
+        values[2 * r + 1] = (double)(-d) * lam;
+    }
+    return OTH_OK;
 }
 
 int oth_td_ema(const double* values, const int64_t* seg_off, const double* init, double a, double one_minus_a,

@@ -37,6 +37,7 @@ SIGNATURES = {
     "oth_replay": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_replay_rows": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_book_text": (_I, [_P, _P, _I64, _P, _P]),
+    "oth_book_parse": (_I, [_P, _I64, _P, _P, _I64, _P]),
     "oth_features": (_I, [_P, _P, _P, _I64, _P]),
     "oth_rollout_eval": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_rollout_match": (_I, [_P, _P, _U64, _U64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
@@ -44,6 +45,7 @@ SIGNATURES = {
     "oth_eval": (_I, [_P, _P, _P, _P, _I64, _P]),
     "oth_td_updates": (_I, [_P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_updates_rows": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "oth_td_updates_records": (_I, [_P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),
     "oth_td_ema_split": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64, _P]),
     "oth_td_sort_pairs": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),

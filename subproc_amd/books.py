@@ -14,13 +14,81 @@ learners consume GPU games unchanged.
 The positions come from the HIP replay kernel (``ops.replay_rows``) and the text from
 the HIP serializer (``ops.book_text``); only the file assembly (headers,
 slicing per game) is host work.  Redis/DynamoDB I/O itself stays out of scope.
+
+The reader's side (books from any source, e.g. the reference's own Edax
+matches): ``parse_book_strings`` turns records' board strings into bitboards
+with the HIP parser (``ops.book_parse``, board_from_a_book of parameter.py:5-8)
+and ``read_flat_file`` a FlatFileRecorder file; td.StateMap.update_from_records
+feeds such books to the learner.
 """
 import os
 
+import numpy as np
 import torch
 
-from . import ops
+from . import codec, ops
 from ._lib import BOOK_LINE, MOVES_STRIDE
+
+# Board() (board.py:22-27) as serialize_board writes it: Board.deserialize
+# writes a string over a fresh Board, so the squares a short string does not
+# reach keep these characters
+_OPEN_BLACK, _OPEN_WHITE = 0x0000000810000000, 0x0000001008000000
+OPENING_BOOK = codec.serialize_board(_OPEN_BLACK, _OPEN_WHITE)
+
+
+def pack_book_strings(strings):
+    """The 64 bytes Board.deserialize reads from each board string onto a
+    fresh Board (board.py:253-258), concatenated (numpy uint8, 64 per string):
+    a string of 64 characters as it is; a shorter one completed with the
+    opening's characters for the squares it does not reach; a longer one raises
+    IndexError as the reference does (its 65th character indexes row 8).  Any
+    character other than 'O' and 'X' reads as Empty (turn_from_string), so a
+    character outside latin-1 is stored as '?'."""
+    parts = []
+    for s in strings:
+        if len(s) > 64:
+            raise IndexError("list index out of range")
+        parts.append(s if len(s) == 64 else s + OPENING_BOOK[len(s):])
+    return np.frombuffer("".join(parts).encode("latin-1", "replace"), dtype=np.uint8)
+
+
+def parse_book_strings(strings, device="cuda"):
+    """board_from_a_book's board (parameter.py:5-8) of each string, parsed on
+    the GPU: (n, 2) int64 [black, white] on ``device``."""
+    packed = pack_book_strings(strings)
+    n = packed.size // 64
+    if n == 0:
+        return torch.empty((0, 2), dtype=torch.int64, device=device)
+    text = torch.from_numpy(packed.copy()).to(device)
+    return ops.book_parse(text, n)[0]
+
+
+def read_flat_file(path, device="cuda"):
+    """A FlatFileRecorder file (game_recorder.py:67-76) back into the game:
+    returns (black_name, white_name, boards (n, 2) int64, turn (n,) uint8) on
+    ``device``, the body's serialize_str lines parsed in place by the HIP
+    parser (stride OTH_BOOK_LINE)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    head = []
+    for _ in range(2):
+        nl = data.index(b"\n")
+        head.append(data[:nl].decode("latin-1"))
+        data = data[nl + 1:]
+    names = []
+    for line, tag in zip(head, ("% Black: ", "% White: ")):
+        if not line.startswith(tag):
+            raise ValueError("not a FlatFileRecorder file: %r" % line)
+        names.append(line[len(tag):])
+    if len(data) % BOOK_LINE:
+        raise ValueError("the body is not a whole number of %d-byte serialize_str lines" % BOOK_LINE)
+    n = len(data) // BOOK_LINE
+    if n == 0:
+        return names[0], names[1], torch.empty((0, 2), dtype=torch.int64, device=device), \
+            torch.empty(0, dtype=torch.uint8, device=device)
+    text = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).to(device)
+    boards, turn = ops.book_parse(text, n, stride=BOOK_LINE, want_turn=True)
+    return names[0], names[1], boards, turn
 
 
 class GameBooks:

@@ -1184,6 +1184,55 @@ __global__ __launch_bounds__(kBlock) void book_text_kernel(const u64* __restrict
     }
 }
 
+// Book ingest: the reader's side of the same format (game_reader.py,
+// replearn.learn_books) -- board strings back into bitboards, one lane per
+// string.  Four characters at a time: the bytes of a dword equal to 'O' (or
+// 'X') are found with the exact zero-byte test (t = w ^ "OOOO": a byte of t is
+// zero iff its high bit stays clear in ((t & 0x7F..) + 0x7F..) | t), and their
+// four flags are gathered into four consecutive bits.
+__device__ __forceinline__ u32 chars_eq4(u32 w, u32 c4) {
+    const u32 t = w ^ c4;
+    const u32 q = (~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u) >> 7;  // bits 0, 8, 16, 24
+    return (q | (q >> 7) | (q >> 14) | (q >> 21)) & 0xFu;
+}
+__device__ __forceinline__ u32 side_of_char(u32 c) { return c == 'O' ? OTH_BLACK : (c == 'X' ? OTH_WHITE : 0u); }
+// Strings at a stride that is not a multiple of 16 (the 67-byte lines of a
+// flat file) are read byte by byte: 4.1 TB/s over the lines of 262,144 games.
+// Staging each wave's 64-line span through LDS with 16-B loads and
+// funnel-shifting each lane's 17 dwords out of it (the mirror of
+// book_text_kernel's exchange) measured slower, 3.6 TB/s.
+__global__ __launch_bounds__(kBlock) void book_parse_kernel(const uint8_t* __restrict__ text, int64_t stride,
+                                                            u64* __restrict__ boards, uint8_t* __restrict__ turn,
+                                                            int64_t n, int vec) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* s = text + i * stride;
+    u32 w[16];
+    if (vec) {  // 16-B aligned strings: four dwordx4 loads
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 v = reinterpret_cast<const uint4*>(s)[q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            w[k] = (u32)s[4 * k] | (u32)s[4 * k + 1] << 8 | (u32)s[4 * k + 2] << 16 | (u32)s[4 * k + 3] << 24;
+    }
+    u32 b[2] = {0, 0}, x[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        b[k >> 3] |= chars_eq4(w[k], 0x4F4F4F4Fu) << (4 * (k & 7));  // 'O'
+        x[k >> 3] |= chars_eq4(w[k], 0x58585858u) << (4 * (k & 7));  // 'X'
+    }
+    reinterpret_cast<ulonglong2*>(boards)[i] =
+        make_ulonglong2(((u64)b[1] << 32) | b[0], ((u64)x[1] << 32) | x[0]);
+    if (turn) turn[i] = (uint8_t)side_of_char(s[65]);
+}
+
 // ---------------------------------------------------------------------------
 // §8f row 2: learner features, counts() of parameter_progress_position_moves_learn.py:5-17:
 // (64 - n_empty, n_puttable_for(side), mask_count(side, m) for the 8 region masks)
@@ -1277,6 +1326,28 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     vals[j] = (double)vb * lam;
     keys[j + 1] = td_key(b, OTH_WHITE);
     vals[j + 1] = (double)(-vb) * lam;
+}
+
+// one thread per book record, in the learner's own order: row r is update
+// pair 2r ('O') and 2r + 1 ('X'); its book's terminal record (book[0]) is row
+// term_row[r] and l ** turn_left is lam_pow[lam_idx[r]]
+__global__ __launch_bounds__(kBlock) void td_records_kernel(const u64* __restrict__ rows,
+                                                            const int64_t* __restrict__ term_row,
+                                                            const int32_t* __restrict__ lam_idx,
+                                                            const double* __restrict__ lam_pow,
+                                                            int64_t* __restrict__ keys, double* __restrict__ vals,
+                                                            int64_t n) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n) return;
+    const ulonglong2* rb = reinterpret_cast<const ulonglong2*>(rows);
+    const ulonglong2 term = rb[term_row[r]];
+    const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
+    const double lam = lam_pow[lam_idx[r]];
+    const ulonglong2 b = rb[r];
+    keys[2 * r] = td_key(b, OTH_BLACK);
+    vals[2 * r] = (double)vb * lam;
+    keys[2 * r + 1] = td_key(b, OTH_WHITE);
+    vals[2 * r + 1] = (double)(-vb) * lam;
 }
 
 // one thread per key segment, strictly sequential in stream order (the EMA is
@@ -1789,6 +1860,15 @@ int oth_book_text(const uint64_t* boards, const uint8_t* turn, int64_t n, char* 
     return launched();
 }
 
+int oth_book_parse(const char* text, int64_t stride, uint64_t* boards, uint8_t* turn, int64_t n, void* stream) {
+    if (n < 0 || stride < 64 || (turn && stride < 66) || (n > 0 && (!text || !boards))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    const int vec = ((uintptr_t)text & 15) == 0 && stride % 16 == 0;
+    book_parse_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(reinterpret_cast<const uint8_t*>(text),
+                                                                        stride, boards, turn, n, vec);
+    return launched();
+}
+
 int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!boards || !side || !out))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
@@ -1824,6 +1904,16 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, row_off, plies,
                                                                                           base, lam_pow, keys, values,
                                                                                           n);
+    return launched();
+}
+
+int oth_td_updates_records(const uint64_t* rows, const int64_t* term_row, const int32_t* lam_idx,
+                           const double* lam_pow, int64_t* keys, double* values, int64_t n_rows, void* stream) {
+    if (n_rows < 0 || (n_rows > 0 && (!rows || !term_row || !lam_idx || !lam_pow || !keys || !values)))
+        return OTH_EINVAL;
+    if (n_rows == 0) return OTH_OK;
+    td_records_kernel<<<blocks_for(n_rows), kBlock, 0, (hipStream_t)stream>>>(rows, term_row, lam_idx, lam_pow, keys,
+                                                                              values, n_rows);
     return launched();
 }
 

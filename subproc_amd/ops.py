@@ -390,6 +390,28 @@ def book_text(boards, turn):
     return out
 
 
+def book_parse(text, n, stride=64, want_turn=False):
+    """Board strings back into bitboards (oth_book_parse): ``text`` a uint8
+    device tensor holding n strings of 64 chars at a stride of ``stride``
+    bytes (64 packed; 67 = OTH_BOOK_LINE for serialize_str lines).  Returns
+    (boards (n, 2) int64, turn (n,) uint8 or None); ``want_turn`` parses the
+    side after each board's space (needs stride >= 66)."""
+    if not isinstance(text, torch.Tensor) or text.dtype != torch.uint8 or text.dim() != 1:
+        raise TypeError("text: expected a 1-D uint8 tensor")
+    if stride < 64 or (want_turn and stride < 66):
+        raise ValueError("stride must be >= 64 (>= 66 to parse the side)")
+    if n < 0 or (n > 0 and text.numel() < (n - 1) * stride + (66 if want_turn else 64)):
+        raise ValueError(f"text holds fewer than {n} strings at stride {stride}")
+    pt = _dev(text, "text", torch.uint8)
+    dev = text.device
+    b = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    t = torch.empty(n, dtype=torch.uint8, device=dev) if want_turn else None
+    with torch.cuda.device(dev):
+        check(_lib.load().oth_book_parse(pt, stride, b.data_ptr(), None if t is None else t.data_ptr(), n, _stream()),
+              "oth_book_parse")
+    return b, t
+
+
 def features(boards, side):
     """counts() of parameter_progress_position_moves_learn.py:5-17 per position
     for side 1 ('O' = Black) / 2 ('X' = White): (n, 10) uint8 =

@@ -80,6 +80,26 @@ def hash_string(k):
     return ":".join(str(v) for v in key_to_counts(k))
 
 
+def records_plan(books, lam=LAMBDA):
+    """The host half of StateMap.update_from_records: the board strings of
+    every record in processing order, and per record the row of its book's
+    terminal record (int64), its index (int32) into a table (float64) of
+    l ** (last_turn - turn) over the distinct exponents, each power computed
+    as the learner computes it (a CPython float power, 46)."""
+    strings, expo, term = [], [], []
+    for _book_id, book, _meta in books:
+        last_turn = int(book[0]["turn"])
+        t0 = len(strings)
+        for rec in book:
+            strings.append(rec["book"])
+            expo.append(last_turn - int(rec["turn"]))
+            term.append(t0)
+    uniq = sorted(set(expo))
+    slot = {k: i for i, k in enumerate(uniq)}
+    return (strings, np.array(term, np.int64), np.array([slot[k] for k in expo], np.int32),
+            np.array([lam ** k for k in uniq], np.float64))
+
+
 class StateMap:
     """Device-resident 'param:state:*' table: sorted int64 keys + float64 values."""
 
@@ -130,6 +150,48 @@ class StateMap:
                                               plies.contiguous().data_ptr(), base.data_ptr(),
                                               self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n, stream),
                       "oth_td_updates_rows")
+        self._apply(keys, vals)
+        return total
+
+    def update_from_records(self, books):
+        """learn_and_update_batch's state-map half (progress_position_moves_learn.py:94-96
+        -> __update_state_for_a_book, 37-62) over books as replearn.learn_books
+        hands them over (replearn.py:27-46), from any source: ``books`` =
+        [(book_id, records, meta), ...], each record a dict with 'book' (the
+        board string) and 'turn', the terminal record first.  Every record is
+        applied in the given order, sides 'O' then 'X', with its own
+        l ** (last_turn - turn) (gaps, repeats and any order of turns as the
+        reference has them); the board strings are parsed on the GPU
+        (books.parse_book_strings) and the updates built by
+        oth_td_updates_records.  A book without records raises IndexError, a
+        malformed turn ValueError, as in the reference.  Returns the number of
+        updates applied."""
+        from .books import parse_book_strings
+        strings, term, lam_idx, lam_pow = records_plan(books, self.lam)
+        if not strings:
+            return 0
+        rows = parse_book_strings(strings, self.device)
+        lam_pow = torch.from_numpy(lam_pow).to(self.device)
+        lam_idx = torch.from_numpy(lam_idx).to(self.device)
+        term_row = torch.from_numpy(term).to(self.device)
+        total = 2 * len(strings)
+        keys = torch.empty(total, dtype=torch.int64, device=self.device)
+        vals = torch.empty(total, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(_lib.load().oth_td_updates_records(rows.data_ptr(), term_row.data_ptr(), lam_idx.data_ptr(),
+                                                     lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(),
+                                                     len(strings), torch.cuda.current_stream(self.device).cuda_stream),
+                  "oth_td_updates_records")
+        self._apply(keys, vals)
+        return total
+
+    def _apply(self, keys, vals):
+        """The batch's ordered (key, value) update stream into the table:
+        stable sort by key, each key's EMA in stream order, merge."""
+        total = keys.numel()
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
             sk, sv = torch.empty_like(keys), torch.empty_like(vals)
             tb = ctypes.c_size_t(0)
             check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total, None,
@@ -161,7 +223,6 @@ class StateMap:
                 self.keys, self.values = ukeys, out
             else:
                 self._merge(is_new, ukeys, out, lib, stream)
-        return total
 
     def _merge(self, is_new, ukeys, out, lib, stream):
         """The batch's keys (sorted, unique; is_new: absent from the table) into

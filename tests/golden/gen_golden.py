@@ -22,6 +22,7 @@ second independent implementation.
 Usage:  python tests/golden/gen_golden.py        (≈1–2 min on 8 cores)
 """
 import json
+import random
 import multiprocessing as mp
 import os
 import sys
@@ -926,10 +927,87 @@ def batch_stats_fixtures():
     print("batch_stats.json:", len(cases), "cases;", len(slack.messages), "slack messages captured")
 
 
+def td_records_fixtures():
+    """The learner's state-map update over books that are not clean GameRunner
+    games (books read from any store: td.StateMap.update_from_records).
+    __update_state_for_a_book / __update_state_map
+    (progress_position_moves_learn.py:37-62) over each book in the given order:
+    the key is the reference's own hash_from_book, the terminal value its
+    board_from_a_book (both exec'd against the shimmed board.py), and the five
+    EMA lines are restated as for td_state.npz (the module imports pyres and
+    slack).  Books are built from rollout_random.npz games replayed through
+    board.py, then altered: records dropped (gaps in turn), repeated, shuffled
+    after the terminal, turns as strings, board strings cut short (the rest of
+    the squares stay the opening's) or holding other characters ('o', 'x',
+    '.', ...: Empty), and boards of random characters."""
+    ns = load_reference_counts(want_ns=True)
+    param = ns["ProgressPositionMovesParameter"]()
+    bfab = ns["board_from_a_book"]
+    a_, l_ = 0.03, 0.90  # ProgressPositionMovesLearn.__init__ (22-24)
+    z = np.load(os.path.join(OUT, "rollout_random.npz"))
+    ib, iw = to_bits(Board())
+
+    def game_book(g):
+        b = from_bits(ib, iw, Black)
+        recs = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn, "end": b.is_game_over()}]
+        for code in z["moves"][g]:
+            if code == 255:
+                break
+            assert b.put_s(code_to_str(b, int(code))) >= 0
+            recs.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                         "end": b.is_game_over()})
+        return list(reversed(sorted(recs, key=lambda x: int(x["turn"]))))  # learn_books' order
+
+    rnd = random.Random(20261017)
+    books, kinds = [], []
+    for g in range(40):
+        book = game_book(g)
+        kind = ["clean", "gaps", "repeats", "shuffled", "str_turns", "short", "chars", "random_boards"][g % 8]
+        if kind == "gaps":
+            book = [book[0]] + [r for r in book[1:] if rnd.random() < 0.6]
+        elif kind == "repeats":
+            book = [book[0]] + [r for r in book[1:] for _ in range(1 + (rnd.random() < 0.3))]
+        elif kind == "shuffled":
+            rest = book[1:]
+            rnd.shuffle(rest)
+            book = [book[0]] + rest
+        elif kind == "str_turns":
+            book = [dict(r, turn=str(r["turn"])) for r in book]
+        elif kind == "short":
+            book = [dict(r, book=r["book"][:rnd.randrange(0, 65)]) for r in book]
+        elif kind == "chars":
+            book = [dict(r, book="".join(c if rnd.random() < 0.8 else rnd.choice("ox.* #0") for c in r["book"]))
+                    for r in book]
+        elif kind == "random_boards":
+            book = [dict(r, book="".join(rnd.choice("OX-OX-ox.") for _ in range(64))) for r in book]
+        books.append(book)
+        kinds.append(kind)
+    store = {}
+    for book in books:  # learn_and_update_batch (94-96) -> __update_state_for_a_book (37-48)
+        last_turn = int(book[0]["turn"])
+        last_board = bfab(book[0])
+        vb = last_board.n_black() - last_board.n_white()
+        vw = last_board.n_white() - last_board.n_black()
+        for rec in book:
+            for side, value in (("O", vb), ("X", vw)):
+                key = param.hash_from_book(rec, side)
+                cur = float(store.get(key, 0))
+                new = float(value) * (l_ ** (last_turn - int(rec["turn"])))
+                store[key] = new if cur == 0 else cur * (1 - a_) + new * a_
+    ks = sorted(store)
+    out = {"source": "progress_position_moves_learn.py:37-62 over rollout_random.npz games replayed through "
+                     "board.py and altered; hash_from_book / board_from_a_book exec'd from the reference",
+           "kinds": kinds, "books": books, "hash": ks, "value": [store[k] for k in ks]}
+    json.dump(out, open(os.path.join(OUT, "td_records.json"), "w"))
+    print("td_records.json:", len(books), "books,", sum(map(len, books)), "records,", len(ks), "keys")
+
+
 if __name__ == "__main__":
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     if only == "batch_stats":
         batch_stats_fixtures()
+    elif only == "td_records":
+        td_records_fixtures()
     elif only == "runner":
         runner_fixtures(mp.Pool(8))
         print("runner fixtures written to", OUT)

@@ -26,53 +26,33 @@ namespace {
 constexpr int kMergeBlock = 256;
 constexpr int kMergeK = 8;                               // merged positions per thread
 constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
-// the lookup keeps no values in LDS: twice the tile (measured 0.50 against 0.58
-// ms at 8 per thread, where the merge is best at 8: 0.82 against 0.93 ms at 16)
-constexpr int kLookupK = 16;
+constexpr int kLookupK = 8;
 constexpr int kLookupTile = kMergeBlock * kLookupK;
 
-// The merge-path splits of the tile's two ends, found together by the block:
-// for diagonal d the split is the first i in [lo, hi] with A[i] >= B[d-i-1]
-// (A[i] < B[d-i-1] holds below it, fails from it on).  Each half of the block
-// searches one end: every round each of its nt threads probes one of nt evenly
-// spaced indices, and the count of probes that hold narrows the range to one
-// gap; a range of at most nt indices is probed at unit steps, which gives the
-// split.  ~4 rounds for 10^8 keys, instead of 27 dependent loads by one
-// thread.  Block-uniform: every thread runs every round.
-template <typename Key>
-__device__ void coop_splits(const Key* A, int64_t nA, const Key* B, int64_t nB, int64_t d0, int64_t d1,
-                            int64_t* split, int* cnt) {
-    const int nt = (int)blockDim.x / 2, g = (int)threadIdx.x / nt, t = (int)threadIdx.x - g * nt;
-    const int64_t d = g ? d1 : d0;
+// The merge-path splits of every tile, one thread each, in a kernel of their
+// own (the partition step of a merge path): split[s] is the first i in
+// [max(0, d - nB), min(d, nA)] with A[i] >= B[d - i - 1] for diagonal
+// d = min(s * tile, nA + nB) (A[i] < B[d - i - 1] holds below it, fails from
+// it on), by a binary search of ~log2(n) dependent loads.  Round 2 searched
+// inside each tile's block, cooperatively (~4 rounds of 128 probes per end,
+// to avoid one thread's chain of dependent loads): every probe a random line,
+// ~2,000 per block, which made the HBM traffic of the lookup and the merge
+// 3-4x their algorithmic bytes (profiles/r03_profile_summary.json before
+// this change).  Here all the searches run at once, ~25 loads each.
+__global__ __launch_bounds__(kMergeBlock) void td_splits_kernel(const int64_t* __restrict__ A, int64_t nA,
+                                                                const int64_t* __restrict__ B, int64_t nB,
+                                                                int64_t tile, int64_t nsplit,
+                                                                int64_t* __restrict__ split) {
+    const int64_t t = (int64_t)blockIdx.x * kMergeBlock + threadIdx.x;
+    if (t >= nsplit) return;
+    const int64_t d = min(t * tile, nA + nB);
     int64_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
-    bool done = false;
-    for (;;) {
-        const int64_t span = hi - lo;
-        const bool fine = span <= nt;
-        bool holds = false;
-        if (!done && span > 0) {
-            const int64_t i = fine ? lo + t : lo + span * (t + 1) / (nt + 1);
-            holds = (!fine || t < span) && A[i] < B[d - i - 1];
-        }
-        if (threadIdx.x == 0) cnt[0] = cnt[1] = 0;
-        __syncthreads();
-        if (holds) atomicAdd(&cnt[g], 1);
-        __syncthreads();
-        const int c = cnt[g];
-        if (!done) {
-            if (fine) {  // (span 0 included: c = 0)
-                if (t == 0) split[g] = lo + c;
-                done = true;
-            } else {
-                // probes 0..c-1 hold and probe c fails: the split is in (p(c-1), p(c)]
-                const int64_t nlo = c > 0 ? lo + span * c / (nt + 1) + 1 : lo;
-                const int64_t nhi = c < nt ? lo + span * (c + 1) / (nt + 1) : hi;
-                lo = nlo;
-                hi = nhi;
-            }
-        }
-        if (__syncthreads_and(done)) return;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (A[mid] < B[d - mid - 1]) lo = mid + 1;
+        else hi = mid;
     }
+    split[t] = lo;
 }
 
 // Merge path over the table (A: old keys, unique, sorted) and the batch's keys
@@ -90,24 +70,22 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
                                                                const int64_t* __restrict__ B,
                                                                const double* __restrict__ Bv,
                                                                const int64_t* __restrict__ new_before, int64_t nB,
+                                                               const int64_t* __restrict__ split,
                                                                int64_t* __restrict__ out_k,
                                                                double* __restrict__ out_v) {
     __shared__ int64_t sk[kMergeTile];
     __shared__ double sv[kMergeTile];
-    __shared__ int64_t split[2];
-    __shared__ int cnt[2];
     __shared__ unsigned long long range[2];  // min slot, max slot + 1 of the block's outputs
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
     const int64_t d1 = d0 + kMergeTile < nA + nB ? d0 + kMergeTile : nA + nB;
-    coop_splits(A, nA, B, nB, d0, d1, split, cnt);  // threads 0..127: the tile's start, 128..255: its end
     if (tid == 0) {
         range[0] = ~0ull;
         range[1] = 0;
     }
-    __syncthreads();
-    const int64_t a0 = split[0], b0 = d0 - a0;
-    const int na = (int)(split[1] - a0), nb = (int)(d1 - split[1] - b0);
+    const int64_t s0 = split[blockIdx.x], s1 = split[blockIdx.x + 1];  // the tile's ends in A
+    const int64_t a0 = s0, b0 = d0 - a0;
+    const int na = (int)(s1 - a0), nb = (int)(d1 - s1 - b0);
     for (int k = tid; k < na; k += kMergeBlock) {
         sk[k] = A[a0 + k];
         sv[k] = Av[a0 + k];
@@ -186,22 +164,26 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
 
 // The batch's keys (B) looked up in the table (A) by the same merge path:
 // a batch key at merged position m has the m - j table keys below it taken
-// before it, and is in the table iff the next table key equals it.  Every
-// batch key is written once, by the thread whose positions hold it.
+// before it, and is in the table iff the next table key equals it.  The
+// tile's batch keys are one contiguous range of B: their init values and
+// is_new flags are staged in LDS and written by the block with coalesced
+// stores (a thread's own stores, 8 scattered bytes per lane per step, wrote
+// ~5x the bytes they held).
 __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* __restrict__ A,
                                                                 const double* __restrict__ Av, int64_t nA,
                                                                 const int64_t* __restrict__ B, int64_t nB,
+                                                                const int64_t* __restrict__ split,
                                                                 double* __restrict__ init,
                                                                 uint8_t* __restrict__ is_new) {
     __shared__ int64_t sk[kLookupTile];
-    __shared__ int64_t split[2];
-    __shared__ int cnt[2];
+    __shared__ double sinit[kLookupTile];
+    __shared__ uint8_t snew[kLookupTile];
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kLookupTile;
     const int64_t d1 = d0 + kLookupTile < nA + nB ? d0 + kLookupTile : nA + nB;
-    coop_splits(A, nA, B, nB, d0, d1, split, cnt);
-    const int64_t a0 = split[0], b0 = d0 - a0;
-    const int na = (int)(split[1] - a0), nb = (int)(d1 - split[1] - b0);
+    const int64_t s0 = split[blockIdx.x], s1 = split[blockIdx.x + 1];
+    const int64_t a0 = s0, b0 = d0 - a0;
+    const int na = (int)(s1 - a0), nb = (int)(d1 - s1 - b0);
     for (int k = tid; k < na; k += kMergeBlock) sk[k] = A[a0 + k];
     for (int k = tid; k < nb; k += kMergeBlock) sk[na + k] = B[b0 + k];
     __syncthreads();
@@ -223,9 +205,14 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
         const int64_t key = sk[na + j], ai = a0 + i;
         const int64_t next = i < na ? sk[i] : (ai < nA ? A[ai] : -1);
         const bool hit = next == key;
-        init[b0 + j] = hit ? Av[ai] : 0.0;
-        is_new[b0 + j] = hit ? 0 : 1;
+        sinit[j] = hit ? Av[ai] : 0.0;
+        snew[j] = hit ? 0 : 1;
         j++;
+    }
+    __syncthreads();
+    for (int k = tid; k < nb; k += kMergeBlock) {
+        init[b0 + k] = sinit[k];
+        is_new[b0 + k] = snew[k];
     }
 }
 
@@ -305,6 +292,20 @@ __global__ __launch_bounds__(kFitBlock) void td_fit_pass2_kernel(const int64_t* 
     block_sum_to_row(acc, partials + (int64_t)blockIdx.x * OTH_TD_FIT_COLS, lds);
 }
 
+// the tiles' merge-path splits (tiles + 1 of them) into a stream-ordered
+// scratch allocation the caller frees on the same stream after its kernel
+hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t nB, int64_t tile, int64_t tiles,
+                        int64_t** split, hipStream_t stream) {
+    const int64_t ns = tiles + 1;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(split), (size_t)ns * sizeof(int64_t), stream);
+    if (e != hipSuccess) return e;
+    td_splits_kernel<<<(unsigned)((ns + kMergeBlock - 1) / kMergeBlock), kMergeBlock, 0, stream>>>(A, nA, B, nB, tile,
+                                                                                                  ns, *split);
+    e = hipGetLastError();
+    if (e != hipSuccess) (void)hipFreeAsync(*split, stream);
+    return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -328,10 +329,15 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
         return OTH_EINVAL;
     if (n_upd == 0) return OTH_OK;
     const int64_t n = n_old + n_upd;
-    td_lookup_kernel<<<(unsigned)((n + kLookupTile - 1) / kLookupTile), kMergeBlock, 0, (hipStream_t)stream>>>(
-        old_keys, old_vals, n_old, upd_keys, n_upd, init, is_new);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? OTH_OK : -(int)e;
+    const int64_t tiles = (n + kLookupTile - 1) / kLookupTile;
+    int64_t* split = nullptr;
+    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kLookupTile, tiles, &split, (hipStream_t)stream);
+    if (e != hipSuccess) return -(int)e;
+    td_lookup_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(old_keys, old_vals, n_old, upd_keys,
+                                                                              n_upd, split, init, is_new);
+    e = hipGetLastError();
+    const hipError_t ef = hipFreeAsync(split, (hipStream_t)stream);
+    return e != hipSuccess ? -(int)e : (ef == hipSuccess ? OTH_OK : -(int)ef);
 }
 
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
@@ -350,10 +356,15 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
                                (hipStream_t)stream);
         return e == hipSuccess ? OTH_OK : -(int)e;
     }
-    td_merge_kernel<<<(unsigned)((n + kMergeTile - 1) / kMergeTile), kMergeBlock, 0, (hipStream_t)stream>>>(
-        old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? OTH_OK : -(int)e;
+    const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
+    int64_t* split = nullptr;
+    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kMergeTile, tiles, &split, (hipStream_t)stream);
+    if (e != hipSuccess) return -(int)e;
+    td_merge_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(
+        old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, split, out_keys, out_vals);
+    e = hipGetLastError();
+    const hipError_t ef = hipFreeAsync(split, (hipStream_t)stream);
+    return e != hipSuccess ? -(int)e : (ef == hipSuccess ? OTH_OK : -(int)ef);
 }
 
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,

@@ -125,6 +125,43 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     assert out_v.h.tolist() == [want[k] for k in sorted(want)]
 
 
+@pytest.mark.parametrize("shape", ["below", "above", "runs", "tiny_table"])
+def test_td_merge_pair_skewed(shape):
+    """Merge-path splits at the extremes (oth_td_lookup / oth_td_merge take
+    their tiles' ends from a partition kernel): a batch wholly below or above
+    the table, long alternating runs of each side, and a table of 3 keys
+    against 700,000 batch keys."""
+    rng = np.random.default_rng({"below": 1, "above": 2, "runs": 3, "tiny_table": 4}[shape])
+    if shape == "below":
+        old, upd = np.arange(1 << 20, (1 << 20) + 600_000) * 3, np.arange(0, 300_000) * 2
+    elif shape == "above":
+        old, upd = np.arange(0, 600_000) * 3, (1 << 30) + np.arange(0, 300_000) * 5
+    elif shape == "runs":
+        blocks = np.arange(0, 200) * 100_000
+        old = np.concatenate([b + np.arange(0, 5000 + 37 * i) for i, b in enumerate(blocks[::2])])
+        upd = np.concatenate([b + np.arange(0, 3000 + 11 * i) for i, b in enumerate(blocks[1::2])])
+        upd = np.unique(np.concatenate([upd, rng.choice(old, 20_000, replace=False)]))
+    else:
+        old, upd = np.array([5, 10**9, 10**12]), np.unique(rng.integers(0, 1 << 50, 700_000))
+        upd = np.unique(np.concatenate([upd, [5, 10**12]]))
+    old, upd = old.astype(np.int64), upd.astype(np.int64)
+    ov, uv = rng.normal(size=len(old)), rng.normal(size=len(upd))
+    new = ~np.isin(upd, old)
+    nb = np.concatenate([[0], np.cumsum(new)]).astype(np.int64)
+    ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
+    init, is_new = Buf(np.full(len(upd), 9.0)), Buf(np.full(len(upd), 7, np.uint8))
+    both("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
+    same(init, is_new)
+    np.testing.assert_array_equal(is_new.h, new.astype(np.uint8))
+    n_out = len(old) + int(nb[-1])
+    out_k, out_v = Buf(np.full(n_out, -7, np.int64)), Buf(np.zeros(n_out))
+    both("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
+    same(out_k, out_v)
+    want = dict(zip(old.tolist(), ov.tolist()))
+    want.update(zip(upd.tolist(), uv.tolist()))
+    assert out_k.h.tolist() == sorted(want)
+
+
 @pytest.mark.parametrize("n", [1, 1000, 3_000_001])
 def test_td_fit_moments_pair(n):
     """The regression sums on both builds: the GPU's 1,024 block rows add up to

@@ -1399,7 +1399,7 @@ __device__ __forceinline__ double td_run_full(double v, const double (&b)[kTdChu
 // the rule over vals[i, e) from state v, one thread: short ranges step by
 // step; long ones software-pipelined (a ring of three chunks keeps 2 * kTdChunk
 // loads in flight while the chain consumes the third)
-__device__ double td_range(double v, const double* __restrict__ vals, int64_t i, const int64_t e, double a,
+__device__ __forceinline__ double td_range(double v, const double* __restrict__ vals, int64_t i, const int64_t e, double a,
                            double oma) {
     if (e - i < 3 * kTdChunk) {  // the common case: a handful of updates
         for (; i < e; i++) v = td_step(v, vals[i], a, oma);

@@ -36,7 +36,8 @@ def short(name):
         return "replay_rows_kernel" if m.group(1) == "true" else "replay_kernel"
     for k in ("step_kernel", "legal_kernel", "result_kernel", "reset_kernel", "sample_midgame_kernel",
               "replay_kernel", "book_text_kernel", "book_parse_kernel", "features_kernel", "eval_kernel",
-              "td_updates_kernel", "td_records_kernel", "td_ema_kernel", "td_merge_kernel", "td_lookup_kernel"):
+              "td_updates_kernel", "td_records_kernel", "td_ema_spec_kernel", "td_ema_long_kernel", "td_ema_kernel",
+              "td_merge_kernel", "td_lookup_kernel", "td_splits_kernel"):
         if k in name:
             return k
     return None

@@ -10,9 +10,11 @@
 //
 // The sort:
 // rocPRIM's onesweep radix sort of the pairs themselves over the key's 54 bits
-// (OTH_TD_KEY_BITS): 7 8-bit digit passes of 16-byte pairs.  torch.sort of the
-// keys with a permutation is 8 passes of (key, int64 index) pairs plus a gather
-// of the values by that permutation.
+// (OTH_TD_KEY_BITS), in 6 passes of 9-bit digits (the gfx950 default takes 8
+// bits a pass, 7 passes: 2.11-2.13 against 1.93 ms for 32.2M pairs,
+// tools/diag/sort_bits.hip; 10 bits ran 3.58 ms, 11 do not fit the LDS).
+// torch.sort of the keys with a permutation is 8 passes of (key, int64 index)
+// pairs plus a gather of the values by that permutation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,6 +24,11 @@
 #include "../../include/othello.h"
 
 namespace {
+
+using SortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>>;
 
 constexpr int kMergeBlock = 256;
 constexpr int kMergeK = 8;                               // merged positions per thread
@@ -376,7 +383,7 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
     uint64_t* kout = reinterpret_cast<uint64_t*>(keys_out);
     if (!temp) {  // size query: no work, no launch
         size_t bytes = 0;
-        const hipError_t e = rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
+        const hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
                                                        OTH_TD_KEY_BITS, (hipStream_t)stream);
         *temp_bytes = bytes;
         return e == hipSuccess ? OTH_OK : -(int)e;
@@ -384,7 +391,7 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
     if (n > 0 && (!keys_in || !vals_in || !keys_out || !vals_out)) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
     size_t bytes = *temp_bytes;
-    const hipError_t e = rocprim::radix_sort_pairs(temp, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
+    const hipError_t e = rocprim::radix_sort_pairs<SortConfig>(temp, bytes, kin, kout, vals_in, vals_out, (size_t)n, 0,
                                                    OTH_TD_KEY_BITS, (hipStream_t)stream);
     return e == hipSuccess ? OTH_OK : -(int)e;
 }

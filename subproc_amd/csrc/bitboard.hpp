@@ -350,21 +350,6 @@ __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     return f | rev64(fr);
 }
 
-// flips of the move on empty square sq from the mover's run sets, with the
-// move's rays computed in registers (rays_of) instead of read from the LDS
-// table: the replay, whose LDS holds its output stages
-__device__ __forceinline__ u64 flips_runs(u32 sq, const RunSets& r) {
-    u64 R[kRayRows];
-    rays_of(sq, R);
-    u64 f = east_run(1ull << sq, r.A1);
-    u64 fr = east_run(1ull << (sq ^ 63u), r.rA0);
-    f = or3(f, run_prefix(R[0], r.A3), run_prefix(R[1], r.A5));
-    f |= run_prefix(R[2], r.A7);
-    fr = or3(fr, run_prefix(R[3], r.rA2), run_prefix(R[4], r.rA4));
-    fr |= run_prefix(R[5], r.rA6);
-    return f | rev64(fr);
-}
-
 // legal moves only (no run sets kept) — for child positions / next-state masks
 template <int ORDER = 798>
 __device__ __forceinline__ u64 moves(u64 P, u64 O) {

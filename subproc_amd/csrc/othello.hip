@@ -957,29 +957,28 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                 const u32 c = (u32)(win >> (8 * k)) & 0xffu;
                 const bool fast = t == OTH_BLACK || t == OTH_WHITE;
                 if (pos_end && fast) {
-                    // one analysis of the mover serves is_game_over (the other
-                    // side is analysed only where the mover has no move) and the
-                    // flips of its move (run sets and the move's rays, in registers)
+                    // A recorded move that flips proves the mover can move, so
+                    // the position is not over and only the move's flips are
+                    // needed (flips_carry, ~85 VALU); a pass, an illegal code or
+                    // the last position takes is_game_over the long way (an
+                    // analysis, and the other side's only where the mover has
+                    // no move).  One analysis for both, with the flips from its
+                    // run sets, cost ~165 VALU at every position.
                     const bool black = t == OTH_BLACK;
                     u64 P = black ? bl : wh, O = black ? wh : bl;
-                    Position pm;
-                    analyse(P, O, pm);
+                    u64 f = 0;
+                    if (p < np && c < 64 && !((P | O) >> c & 1ull)) f = flips_carry(c, P, O);
                     u32 e = 0;
-                    if (pm.legal == 0) e = moves_of(O, P) == 0;
+                    if (!f && moves_of(P, O) == 0) e = moves_of(O, P) == 0;
                     put_te(p, t | (e << 7), t);
-                    if (p < np) {
-                        if (c == OTH_PASS) {
-                            t ^= 3u;
-                        } else if (c < 64 && !((P | O) >> c & 1ull)) {
-                            const u64 f = flips_runs(c, run_sets(pm));
-                            if (f) {
-                                P = or3(P, f, 1ull << c);
-                                O = andn(O, f);
-                                bl = black ? P : O;
-                                wh = black ? O : P;
-                                t ^= 3u;
-                            }
-                        }
+                    if (f) {
+                        P = or3(P, f, 1ull << c);
+                        O = andn(O, f);
+                        bl = black ? P : O;
+                        wh = black ? O : P;
+                        t ^= 3u;
+                    } else if (p < np && c == OTH_PASS) {
+                        t ^= 3u;
                     }
                     continue;
                 }

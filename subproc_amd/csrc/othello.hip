@@ -1197,9 +1197,10 @@ __device__ __forceinline__ u32 chars_eq4(u32 w, u32 c4) {
 __device__ __forceinline__ u32 side_of_char(u32 c) { return c == 'O' ? OTH_BLACK : (c == 'X' ? OTH_WHITE : 0u); }
 // Strings at a stride that is not a multiple of 16 (the 67-byte lines of a
 // flat file) are read byte by byte: 4.1 TB/s over the lines of 262,144 games.
-// Staging each wave's 64-line span through LDS with 16-B loads and
-// funnel-shifting each lane's 17 dwords out of it (the mirror of
-// book_text_kernel's exchange) measured slower, 3.6 TB/s.
+// Measured slower: staging each wave's 64-line span through LDS with 16-B
+// loads and funnel-shifting each lane's 17 dwords out of it (the mirror of
+// book_text_kernel's exchange), 3.6 TB/s; the lane's 17 covering dwords
+// loaded straight from memory and funnel-shifted, 3.2-3.3 TB/s.
 __global__ __launch_bounds__(kBlock) void book_parse_kernel(const uint8_t* __restrict__ text, int64_t stride,
                                                             u64* __restrict__ boards, uint8_t* __restrict__ turn,
                                                             int64_t n, int vec) {

@@ -498,6 +498,23 @@ struct RolloutArgs {
 __device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
 #endif
 
+// Move records of the random policy (RECORD): a lane's record is one 128-byte
+// row and the batch's 64 games are consecutive, so the wave's records are one
+// contiguous 8 KB span.  They are built in LDS (row stride 132 bytes, 33
+// dwords: a ply's byte stores from the 64 lanes fall in different banks) and
+// written out after the batch by 16-byte stores, 1 KB per wave instruction.
+// Stored a byte per lane per ply straight to memory, the records' lines were
+// written partially, again and again: 0.74-0.77 GB of HBM traffic per
+// 262,144-game launch for 38 MB of output (profiles/r03_profile_summary.json).
+#ifndef OTH_REC_ALL
+#define OTH_REC_ALL 0
+#endif
+constexpr int kRecStride = OTH_MOVES_STRIDE + 4;
+constexpr int kRecWaveBytes = 64 * kRecStride;
+constexpr size_t rec_stage_bytes(int policy, bool record) {
+    return record && (OTH_REC_ALL || policy == OTH_POLICY_RANDOM) ? (size_t)(kBlock / 64) * kRecWaveBytes : 0;
+}
+
 template <int POLICY, bool RECORD, bool RUNNER = false>
 __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
@@ -527,6 +544,10 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     const int lane = lane_id();
     const u64 n = (u64)a.n;
     u64 plies_sum = 0;
+    constexpr bool kRecStage = RECORD && (OTH_REC_ALL || POLICY == OTH_POLICY_RANDOM);
+    extern __shared__ u32 rec_dyn[];  // kRecStage: the block's waves' record stages
+    uint8_t* const rec_wave = reinterpret_cast<uint8_t*>(rec_dyn) + (threadIdx.x >> 6) * kRecWaveBytes;
+    uint8_t* const rec_row = rec_wave + lane * kRecStride;
 
     for (;;) {
         // ---- dequeue a batch of 64 games (one per lane)
@@ -553,12 +574,22 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 P = side == OTH_BLACK ? s0.x : s0.y;
                 O = side == OTH_BLACK ? s0.y : s0.x;
             }
-            if (RECORD) {
+            if (RECORD && !kRecStage) {
                 uint4* mrec = reinterpret_cast<uint4*>(a.moves + g * OTH_MOVES_STRIDE);
 #pragma unroll
                 for (int q = 0; q < OTH_MOVES_STRIDE / 16; q++) mrec[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
             }
         }
+        if constexpr (kRecStage) {  // the row starts 255-padded
+#pragma unroll
+            for (int q = 0; q < OTH_MOVES_STRIDE / 4; q++) reinterpret_cast<u32*>(rec_row)[q] = ~0u;
+        }
+        // a move code into game g's record (RECORD)
+        auto rec_put = [&](u32 i, uint8_t code) {
+            if (i >= OTH_MOVES_STRIDE) return;
+            if constexpr (kRecStage) rec_row[i] = code;
+            else a.moves[g * OTH_MOVES_STRIDE + i] = code;
+        };
 
         // ---- play the batch: one env-step per active lane per iteration
         if constexpr (POLICY == OTH_POLICY_RANDOM) {
@@ -599,7 +630,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         return true;
                     }
                     // the mover must pass ('PS'): hand the move over
-                    if (RECORD && npass < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + npass] = OTH_PASS;
+                    if (RECORD) rec_put(npass, OTH_PASS);
                     passed = true;
                     npass++;
                     return false;
@@ -609,7 +640,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 const u64* col = ray_col(rays, off);
                 const Flips f = flips_col(col[kRayRows * 64], run_sets(pos), col);
                 if (RECORD) {
-                    if (npass < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + npass] = (uint8_t)(off >> 3);
+                    rec_put(npass, (uint8_t)(off >> 3));
                     npass++;
                 }
                 place(X, Y, f);
@@ -621,7 +652,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     if (ply_of(O, P)) break;
                 }
                 const u32 ply = RECORD ? npass : (u32)__popcll(P | O) - discs0 + npass;
-                if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = 0xFF;
+                if (RECORD) rec_put(ply, 0xFF);
                 const u64 bl = b0 ? P : O, wh = b0 ? O : P;
                 const int d = __popcll(bl) - __popcll(wh);
                 if (a.final_boards) reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
@@ -677,7 +708,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         }
                     } else {
                         if (passed) {
-                            if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = OTH_PASS;
+                            if (RECORD) rec_put(ply, OTH_PASS);
                             ply++;
                             passed = false;
                             if (RUNNER) {  // the passer's turn drew its coin (go_for, game_runner.py:134-135)
@@ -710,7 +741,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 if (moving) {
                     const Flips f = flips_rays(sq, run_sets(pos), rays);
-                    if (RECORD && ply < OTH_MOVES_STRIDE) a.moves[g * OTH_MOVES_STRIDE + ply] = (uint8_t)sq;
+                    if (RECORD) rec_put(ply, (uint8_t)sq);
                     place(P, O, f);
                     const u64 np = O;
                     O = P;
@@ -719,6 +750,17 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                     ply++;
                 }
             }
+        }
+        if constexpr (kRecStage) {  // the wave's records, one contiguous span, 16 bytes a lane
+            wave_sync();
+            const int nvalid = (int)min<u64>(64, n - base);
+            for (int c = lane; c < nvalid * (OTH_MOVES_STRIDE / 16); c += 64) {
+                const int j = c / (OTH_MOVES_STRIDE / 16), part = c % (OTH_MOVES_STRIDE / 16);
+                const u32* src = reinterpret_cast<const u32*>(rec_wave + j * kRecStride + part * 16);
+                reinterpret_cast<uint4*>(a.moves + (base + j) * OTH_MOVES_STRIDE)[part] =
+                    make_uint4(src[0], src[1], src[2], src[3]);
+            }
+            wave_sync();  // read out before the next batch pads the rows again
         }
     }
 
@@ -1764,20 +1806,21 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     hipStream_t st = (hipStream_t)stream;
     if (run) {
         if (policy == OTH_POLICY_EVAL) {
-            if (moves) rollout_kernel<OTH_POLICY_EVAL, true, true><<<grid, kBlock, 0, st>>>(a);
+            if (moves) rollout_kernel<OTH_POLICY_EVAL, true, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_EVAL, true), st>>>(a);
             else rollout_kernel<OTH_POLICY_EVAL, false, true><<<grid, kBlock, 0, st>>>(a);
         } else {
-            if (moves) rollout_kernel<OTH_POLICY_GREEDY, true, true><<<grid, kBlock, 0, st>>>(a);
+            if (moves) rollout_kernel<OTH_POLICY_GREEDY, true, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_GREEDY, true), st>>>(a);
             else rollout_kernel<OTH_POLICY_GREEDY, false, true><<<grid, kBlock, 0, st>>>(a);
         }
     } else if (policy == OTH_POLICY_EVAL) {
-        if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
+        if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_EVAL, true), st>>>(a);
         else rollout_kernel<OTH_POLICY_EVAL, false><<<grid, kBlock, 0, st>>>(a);
     } else if (policy == OTH_POLICY_GREEDY) {
-        if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, 0, st>>>(a);
+        if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_GREEDY, true), st>>>(a);
         else rollout_kernel<OTH_POLICY_GREEDY, false><<<grid, kBlock, 0, st>>>(a);
     } else {
-        if (moves) rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, 0, st>>>(a);
+        if (moves)
+            rollout_kernel<OTH_POLICY_RANDOM, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_RANDOM, true), st>>>(a);
         else rollout_kernel<OTH_POLICY_RANDOM, false><<<grid, kBlock, 0, st>>>(a);
     }
     return launched();

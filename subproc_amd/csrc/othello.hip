@@ -503,16 +503,17 @@ __device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime),
 // contiguous 8 KB span.  They are built in LDS (row stride 132 bytes, 33
 // dwords: a ply's byte stores from the 64 lanes fall in different banks) and
 // written out after the batch by 16-byte stores, 1 KB per wave instruction.
+// (The 1-ply policies keep their direct stores: their kernels are VALU-bound
+// and hide them, 0.72 ms per 262,144 greedy games with or without records,
+// while the 33 KB stage would halve their resident blocks: 0.83 ms with it,
+// eval 1.17 -> 1.46 ms; tools/diag/record_policies.py.)
 // Stored a byte per lane per ply straight to memory, the records' lines were
 // written partially, again and again: 0.74-0.77 GB of HBM traffic per
 // 262,144-game launch for 38 MB of output (profiles/r03_profile_summary.json).
-#ifndef OTH_REC_ALL
-#define OTH_REC_ALL 0
-#endif
 constexpr int kRecStride = OTH_MOVES_STRIDE + 4;
 constexpr int kRecWaveBytes = 64 * kRecStride;
 constexpr size_t rec_stage_bytes(int policy, bool record) {
-    return record && (OTH_REC_ALL || policy == OTH_POLICY_RANDOM) ? (size_t)(kBlock / 64) * kRecWaveBytes : 0;
+    return record && policy == OTH_POLICY_RANDOM ? (size_t)(kBlock / 64) * kRecWaveBytes : 0;
 }
 
 template <int POLICY, bool RECORD, bool RUNNER = false>
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     const int lane = lane_id();
     const u64 n = (u64)a.n;
     u64 plies_sum = 0;
-    constexpr bool kRecStage = RECORD && (OTH_REC_ALL || POLICY == OTH_POLICY_RANDOM);
+    constexpr bool kRecStage = RECORD && POLICY == OTH_POLICY_RANDOM;
     extern __shared__ u32 rec_dyn[];  // kRecStage: the block's waves' record stages
     uint8_t* const rec_wave = reinterpret_cast<uint8_t*>(rec_dyn) + (threadIdx.x >> 6) * kRecWaveBytes;
     uint8_t* const rec_row = rec_wave + lane * kRecStride;
@@ -1806,17 +1807,17 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     hipStream_t st = (hipStream_t)stream;
     if (run) {
         if (policy == OTH_POLICY_EVAL) {
-            if (moves) rollout_kernel<OTH_POLICY_EVAL, true, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_EVAL, true), st>>>(a);
+            if (moves) rollout_kernel<OTH_POLICY_EVAL, true, true><<<grid, kBlock, 0, st>>>(a);
             else rollout_kernel<OTH_POLICY_EVAL, false, true><<<grid, kBlock, 0, st>>>(a);
         } else {
-            if (moves) rollout_kernel<OTH_POLICY_GREEDY, true, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_GREEDY, true), st>>>(a);
+            if (moves) rollout_kernel<OTH_POLICY_GREEDY, true, true><<<grid, kBlock, 0, st>>>(a);
             else rollout_kernel<OTH_POLICY_GREEDY, false, true><<<grid, kBlock, 0, st>>>(a);
         }
     } else if (policy == OTH_POLICY_EVAL) {
-        if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_EVAL, true), st>>>(a);
+        if (moves) rollout_kernel<OTH_POLICY_EVAL, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_EVAL, false><<<grid, kBlock, 0, st>>>(a);
     } else if (policy == OTH_POLICY_GREEDY) {
-        if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, rec_stage_bytes(OTH_POLICY_GREEDY, true), st>>>(a);
+        if (moves) rollout_kernel<OTH_POLICY_GREEDY, true><<<grid, kBlock, 0, st>>>(a);
         else rollout_kernel<OTH_POLICY_GREEDY, false><<<grid, kBlock, 0, st>>>(a);
     } else {
         if (moves)

@@ -20,8 +20,10 @@
  *
  * Ownership / errors / threading:
  *   - every pointer is DEVICE memory owned by the caller (e.g. torch tensors);
- *     the library allocates nothing and keeps no device state (the rollouts'
- *     work counter is a word the caller passes in, see oth_rollout);
+ *     the library keeps no device state (the rollouts' work counter is a
+ *     word the caller passes in, see oth_rollout) and allocates only a small
+ *     stream-ordered scratch table inside oth_td_lookup / oth_td_merge
+ *     (hipMallocAsync, freed on the same stream);
  *   - calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
  *     and thread-safe on distinct streams; they may be captured in a hipGraph;
  *   - return value: OTH_OK (0), OTH_EINVAL (invalid argument, nothing launched),

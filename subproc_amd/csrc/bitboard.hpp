@@ -49,6 +49,21 @@ __device__ __forceinline__ u64 bitop3(u64 a, u64 b, u64 c) {
 __device__ __forceinline__ u64 bfi(u64 m, u64 a, u64 b) { return bitop3<0xCA>(m, a, b); }
 __device__ __forceinline__ u64 andn(u64 a, u64 b) { return bitop3<0x30>(a, b, b); }
 __device__ __forceinline__ u64 or3(u64 a, u64 b, u64 c) { return bitop3<0xFE>(a, b, c); }
+// Two-input AND / OR as v_bitop3_b32 too (VOP3), not hipcc's v_and/v_or_b32_e32
+// (VOP2).  Measured on the box (tools/diag/valu_rate7.cpp, 8 waves/SIMD): a
+// fast instruction issued among slow VOP3 ones (64-bit shifts,
+// v_lshl_add_u64, v_bcnt) costs ~2.9 cycles in a VOP3 encoding and ~3.6 in
+// a VOP1/VOP2 one, though both stream at ~2.2 alone.
+__device__ __forceinline__ u64 and2(u64 a, u64 b) { return bitop3<0xC0>(a, b, b); }
+__device__ __forceinline__ u64 or2(u64 a, u64 b) { return bitop3<0xFC>(a, b, b); }
+// 32-bit shifts by a constant in their VOP3 encoding (same reason)
+template <int K, bool L>
+__device__ __forceinline__ u32 sh32(u32 x) {
+    u32 r;
+    if (L) asm("v_lshlrev_b32_e64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(K));
+    else asm("v_lshrrev_b32_e64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(K));
+    return r;
+}
 // 64-bit shifts as single v_lshlrev_b64 / v_lshrrev_b64 (inline asm): with
 // the 3-input logic taken apart into 32-bit halves, hipcc's combiner would
 // otherwise split each shift into v_lshlrev_b32 + v_alignbit_b32, two
@@ -70,8 +85,8 @@ template <int S>
 __device__ __forceinline__ PairProp pair_prop(u64 pro) {
     PairProp q;
     q.pro = pro;
-    q.p2L = pro & sh<S, true>(pro);              // q, q-S in pro
-    q.p4L = q.p2L & sh<2 * S, true>(q.p2L);      // q .. q-3S in pro
+    q.p2L = and2(pro, sh<S, true>(pro));          // q, q-S in pro
+    q.p4L = and2(q.p2L, sh<2 * S, true>(q.p2L));  // q .. q-3S in pro
     q.p2R = sh<S, false>(q.p2L);                 // q, q+S in pro
     q.p4R = sh<3 * S, false>(q.p4L);             // q .. q+3S in pro
     return q;
@@ -86,10 +101,10 @@ __device__ __forceinline__ u64 ks_step(u64 gen, u64 pro) {
     if constexpr (K >= 32) {
         u32 lo = (u32)gen, hi = (u32)(gen >> 32);
         if (L) {
-            const u32 s = K == 32 ? lo : lo << (K - 32);
+            const u32 s = K == 32 ? lo : sh32<(K == 32 ? 1 : K - 32), true>(lo);
             hi = (u32)__builtin_amdgcn_bitop3_b32((u32)(pro >> 32), s, hi, 0xCA);
         } else {
-            const u32 s = K == 32 ? hi : hi >> (K - 32);
+            const u32 s = K == 32 ? hi : sh32<(K == 32 ? 1 : K - 32), false>(hi);
             lo = (u32)__builtin_amdgcn_bitop3_b32((u32)pro, s, lo, 0xCA);
         }
         return ((u64)hi << 32) | lo;
@@ -133,9 +148,15 @@ __device__ __forceinline__ u64 east_run(u64 src, u64 Oi) { return andn(Oi, lshl1
 
 // 64-bit bit reversal (two v_bfrev_b32, halves swapped): square sq <-> 63 - sq,
 // which turns the west ray into an east ray.
-__device__ __forceinline__ u64 rev64(u64 x) {
-    return ((u64)__builtin_bitreverse32((u32)x) << 32) | __builtin_bitreverse32((u32)(x >> 32));
+// v_bfrev_b32 in its VOP3 encoding (inline asm; hipcc emits the VOP1 one):
+// a VOP1 slow instruction takes the VOP3 ones after it back to ~3.6 cycles
+// (tools/diag/valu_rate7.cpp)
+__device__ __forceinline__ u32 bfrev32(u32 x) {
+    u32 r;
+    asm("v_bfrev_b32_e64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
 }
+__device__ __forceinline__ u64 rev64(u64 x) { return ((u64)bfrev32((u32)x) << 32) | bfrev32((u32)(x >> 32)); }
 
 // All propagators + attached runs of one position (mover P, opponent O).
 // A[i]: opponent discs reachable from a P disc along direction i through
@@ -154,9 +175,12 @@ struct Position {
 // instead of 2.5, and the bit pairs of 64-bit values make that likely; the
 // order with the fewest such instructions in each kernel's hot loop was picked
 // by tools/valu_mix.py (random rollout: 7-9-8, 11 -> 3 per ply).
-template <int ORDER = 798>
+#ifndef OTH_FILL_ORDER
+#define OTH_FILL_ORDER 798
+#endif
+template <int ORDER = OTH_FILL_ORDER>
 __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
-    const u64 Oi = O & INNER_FILES;
+    const u64 Oi = and2(O, INNER_FILES);
     s.Oi = Oi;
     s.rOi = rev64(Oi);
     // the horizontal pair needs no propagators (carry tricks below)
@@ -173,14 +197,14 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             if (order[k] == 8) {
-                s.A[2] = ks<8, true>(P, v) & O;
-                s.A[3] = ks<8, false>(P, v) & O;
+                s.A[2] = and2(ks<8, true>(P, v), O);
+                s.A[3] = and2(ks<8, false>(P, v), O);
             } else if (order[k] == 9) {
-                s.A[4] = ks<9, true>(P, d9) & O;
-                s.A[5] = ks<9, false>(P, d9) & O;
+                s.A[4] = and2(ks<9, true>(P, d9), O);
+                s.A[5] = and2(ks<9, false>(P, d9), O);
             } else {
-                s.A[6] = ks<7, true>(P, d7) & O;
-                s.A[7] = ks<7, false>(P, d7) & O;
+                s.A[6] = and2(ks<7, true>(P, d7), O);
+                s.A[7] = and2(ks<7, false>(P, d7), O);
             }
         }
     }
@@ -188,7 +212,7 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     u64 m = or3(sh<1, true>(s.A[0]), sh<1, false>(s.A[1]), sh<8, true>(s.A[2]));
     m = or3(m, sh<8, false>(s.A[3]), sh<9, true>(s.A[4]));
     m = or3(m, sh<9, false>(s.A[5]), sh<7, true>(s.A[6]));
-    m |= sh<7, false>(s.A[7]);
+    m = or2(m, sh<7, false>(s.A[7]));
     s.reach = m;
     s.legal = bitop3<0x04>(P, m, O);  // ~P & m & ~O: one v_bitop3_b32 per half
 }
@@ -276,9 +300,9 @@ __device__ __forceinline__ Flips flips_col(u64 mv, const RunSets& r, const u64* 
     u64 f = bitop3<0xBA>(r.A1, lshl1_add(mv, r.A1), mv);     // (A1 & ~(A1 + (mv << 1))) | mv
     u64 fr = bitop3<0xBA>(r.rA0, lshl1_add(rmv, r.rA0), rmv);  // west, in reversed space
     f = or3(f, run_prefix(col[0 * 64], r.A3), run_prefix(col[1 * 64], r.A5));
-    f |= run_prefix(col[2 * 64], r.A7);
+    f = or2(f, run_prefix(col[2 * 64], r.A7));
     fr = or3(fr, run_prefix(col[3 * 64], r.rA2), run_prefix(col[4 * 64], r.rA4));
-    fr |= run_prefix(col[5 * 64], r.rA6);
+    fr = or2(fr, run_prefix(col[5 * 64], r.rA6));
     return Flips{f, rev64(fr)};
 }
 __device__ __forceinline__ Flips flips_rays(u32 sq, const RunSets& r, const u64* tab) {
@@ -324,9 +348,9 @@ __device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
     const u64 lt = (ONES << x) - ONES;        // files < x
     R[0] = 0x0101010101010100ull << sq;                            // +8
     R[1] = andn(0x8040201008040200ull << sq, le);                  // +9: files > x
-    R[2] = (0x0002040810204080ull << sq) & lt;                     // +7: files < x
+    R[2] = and2(0x0002040810204080ull << sq, lt);                  // +7: files < x
     R[3] = 0x0101010101010100ull << rsq;                           // -8
-    R[4] = (0x8040201008040200ull << rsq) & rev64(lt);             // -9: normal files < x
+    R[4] = and2(0x8040201008040200ull << rsq, rev64(lt));          // -9: normal files < x
     R[5] = andn(0x0002040810204080ull << rsq, rev64(le));          // -7: normal files > x
 }
 
@@ -339,19 +363,19 @@ __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     rays_of(sq, R);
     const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
     const u64 rP = rev64(P), rO = rev64(O);
-    const u64 Oi = O & INNER_FILES, rOi = rO & INNER_FILES;
+    const u64 Oi = and2(O, INNER_FILES), rOi = and2(rO, INNER_FILES);
     const u64 se = lshl1_add(mv, Oi), sw = lshl1_add(rmv, rOi);
-    u64 f = (se & P) ? andn(Oi, se) : 0ull;
-    u64 fr = (sw & rP) ? andn(rOi, sw) : 0ull;
+    u64 f = and2(se, P) ? andn(Oi, se) : 0ull;
+    u64 fr = and2(sw, rP) ? andn(rOi, sw) : 0ull;
     f = or3(f, ray_flips(mv << 8, R[0], P, O), ray_flips(mv << 9, R[1], P, O));
     f |= ray_flips(mv << 7, R[2], P, O);
     fr = or3(fr, ray_flips(rmv << 8, R[3], rP, rO), ray_flips(rmv << 9, R[4], rP, rO));
     fr |= ray_flips(rmv << 7, R[5], rP, rO);
-    return f | rev64(fr);
+    return or2(f, rev64(fr));
 }
 
 // legal moves only (no run sets kept) — for child positions / next-state masks
-template <int ORDER = 798>
+template <int ORDER = OTH_FILL_ORDER>
 __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;
     analyse<ORDER>(P, O, s);

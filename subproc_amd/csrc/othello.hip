@@ -100,7 +100,7 @@ __device__ __forceinline__ void eval_weights_to_lds(const EvalWeights& ew, int* 
 __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
     int v = w[0] * (int)__popcll(mob);
 #pragma unroll
-    for (int k = 0; k < 8; k++) v += w[1 + k] * (int)__popcll(mine & kRegionMasks[k]);
+    for (int k = 0; k < 8; k++) v += w[1 + k] * (int)__popcll(and2(mine, kRegionMasks[k]));
     return v;
 }
 
@@ -516,6 +516,12 @@ constexpr size_t rec_stage_bytes(int policy, bool record) {
     return record && policy == OTH_POLICY_RANDOM ? (size_t)(kBlock / 64) * kRecWaveBytes : 0;
 }
 
+// the random loop's fill order (bitboard.hpp analyse): with the VOP3 logic,
+// 7-8-9 leaves the fewest same-bank v_bitop3_b32 in its loop (tools/valu_mix.py)
+#ifndef OTH_RANDOM_FILL_ORDER
+#define OTH_RANDOM_FILL_ORDER 789
+#endif
+constexpr int kRandomFillOrder = OTH_RANDOM_FILL_ORDER;
 template <int POLICY, bool RECORD, bool RUNNER = false>
 __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
@@ -616,7 +622,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 diag_iters++;
 #endif
                 Position pos;
-                analyse(X, Y, pos);
+                analyse<kRandomFillOrder>(X, Y, pos);
                 const u64 legal = pos.legal;
                 // the move count serves the zero test and the pick
                 const u32 c_lo = __popc((u32)legal), nl = c_lo + __popc((u32)(legal >> 32));

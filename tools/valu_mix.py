@@ -44,6 +44,23 @@ MEASURED = {"v_lshlrev_b64": 4.25, "v_lshrrev_b64": 4.22, "v_lshl_add_u64": 4.24
             "v_and_or_b32": 4.11, "v_mov_b64_e32": 4.14, "v_ffbh_u32_e32": 4.05, "v_bfe_u32": 4.20}
 
 
+# Costs inside a mixed loop (tools/diag/valu_rate7.cpp, 8 waves/SIMD, slow
+# VOP3 instructions interleaved with fast ones): a fast instruction costs ~2.95
+# cycles in a VOP3 encoding (v_bitop3_b32, v_and/or_b32_e64) and ~3.7 in a
+# VOP1/VOP2 one (v_and_b32_e32 ...), against 2.2-2.5 when streamed alone; the
+# slow ones keep their isolated cost.  "mean_cycles_mixed" prices a loop so.
+MIXED_FAST_VOP3, MIXED_FAST_E32 = 2.95, 3.7
+
+
+def cycles_mixed(op, line=None):
+    if op == "v_bitop3_b32":
+        return BITOP3_CONFLICT_CYC if bank_conflict(line) else MIXED_FAST_VOP3
+    c = cycles(op, line)
+    if c < 3.0:  # a fast instruction
+        return MIXED_FAST_VOP3 if op.endswith("_e64") else MIXED_FAST_E32
+    return c
+
+
 def bank_conflict(line):
     """three distinct source VGPRs in one bank (v_bitop3_b32 vD, vA, vB, vC)"""
     m = re.match(r"\s*v_bitop3_b32\s+v\d+,\s*v(\d+),\s*v(\d+),\s*v(\d+)", line or "")
@@ -122,9 +139,12 @@ def mix_of(ops, header):
     names = [o for o, _ in ops]
     fast = sum(1 for o in names if FAST.match(o))
     mean = sum(cycles(o, ln) for o, ln in ops) / max(1, len(ops))
+    mixed = sum(cycles_mixed(o, ln) for o, ln in ops) / max(1, len(ops))
     return {"loop_header": header, "valu": len(ops), "fast_vop2": fast, "slow": len(ops) - fast,
             "bitop3_bank_conflicts": sum(1 for o, ln in ops if o == "v_bitop3_b32" and bank_conflict(ln)),
-            "mean_cycles": round(mean, 3), "top": collections.Counter(names).most_common(8)}
+            "e32_fast": sum(1 for o, ln in ops if o.endswith("_e32") and cycles(o, ln) < 3.0),
+            "mean_cycles": round(mean, 3), "mean_cycles_mixed": round(mixed, 3),
+            "top": collections.Counter(names).most_common(8)}
 
 
 def main():
@@ -142,6 +162,7 @@ def main():
                     ops = [(m.group(1), ln) for m, ln in ((re.match(r"^\s+(v_[a-z0-9_]+)", ln), ln) for ln in body) if m]
                     r = mix_of(ops, None)
                 r["peak_winstr_s"] = out["simds"] * out["clock_ghz"] * 1e9 / r["mean_cycles"]
+                r["peak_winstr_s_mixed"] = out["simds"] * out["clock_ghz"] * 1e9 / r["mean_cycles_mixed"]
                 if k == "rollout_kernel<0, false>":
                     r["plies_per_loop_iteration"] = 2  # round 3: the random loop body is two plies
                 out["kernels"][k] = r

@@ -62,6 +62,11 @@ def valu_entry(kernel, achieved, **extra):
          "peak_basis": ("hot-loop mix, %.2f cycles/instr (profiles/valu_mix.json)" % mix["mean_cycles"]) if mix
          else "2 cycles/instr (SIMD-32 issue)",
          "frac_of_2cycle_issue": achieved / VALU_PEAK_HW}
+    if mix and "peak_winstr_s_mixed" in mix:
+        # the same loop priced with the in-mix costs (tools/valu_mix.py mean_cycles_mixed:
+        # a slow VOP3 instruction makes the fast ones after it cost ~2.95 / ~3.7)
+        e["peak_mixed"] = mix["peak_winstr_s_mixed"]
+        e["frac_mixed"] = achieved / mix["peak_winstr_s_mixed"]
     e.update(extra)
     return e
 

@@ -2,12 +2,15 @@
 //
 // Cost model (measured on MI355X, tools/diag/valu_rate*.cpp, DESIGN.md §Cost model):
 // a kernel's throughput is the issue cost of its VALU instructions per env-step.
-// Plain VOP2 logic issues in ~2.2 cycles per wave64, v_bitop3_b32 in ~3.35, and
-// nearly everything else (64-bit shifts, v_bfi/v_or3, v_bcnt, v_cndmask,
-// v_bfrev) in ~4-4.6.  Hence:
+// Streamed alone, bitwise logic issues in ~2.2 cycles per wave64 and nearly
+// everything else (64-bit shifts and adds, v_bfi/v_or3, v_bcnt, v_min,
+// v_bfrev) in ~4-4.4; in these mixed loops a slow instruction costs ~6.5 at the
+// margin and a fast one ~2.9 in a VOP3 encoding but ~3.7 in a VOP1/VOP2 one
+// (tools/diag/valu_rate7.cpp).  Hence:
 //   * 64-bit shifts and adds stay single v_lshl/v_lshrrev_b64 / v_lshl_add_u64;
-//   * all 3-input logic (fill steps, masks, flip accumulation) is one
-//     v_bitop3_b32 per 32-bit half (bitop3, bfi, andn, or3);
+//   * all 2- and 3-input logic (fill steps, masks, flip accumulation) is one
+//     v_bitop3_b32 per 32-bit half (bitop3, bfi, andn, or3, and2, or2), and
+//     the bit reversal and 32-bit shifts are written in their VOP3 forms;
 //   * Kogge-Stone propagators are computed once per position and shared between
 //     opposite directions (p2R = p2L >> S, p4R = p4L >> 3S);
 //   * the chosen move's flips come from per-square ray tables in LDS and the
@@ -412,11 +415,58 @@ __device__ __forceinline__ u32 add_lshl3(u32 a, u32 b) {
 }
 // c_lo = __popc((u32)x), which the caller has from counting x (popcount_lo).
 // Returns 8 x the square: the byte offset of the square's entries in the LDS
-// ray table.  Each level keeps k as min(k, k - c) (the unsigned difference
-// wraps when the bit lies below), the byte is one v_bfe_u32 at the last
+// ray table.  Each level keeps k as k or k - c by the subtraction's borrow
+// (kth_level; formerly min(k, k - c)), the byte is one v_bfe_u32 at the last
 // level's offset, and the three level offsets are disjoint bits (32 | 16 | 8):
 // one v_or3 and one v_add_lshl with the table entry give the offset
 // (31 -> 24 VALU per pick with the address arithmetic).
+#ifndef OTH_PICK_CNDMASK
+#define OTH_PICK_CNDMASK 1
+#endif
+#if OTH_PICK_CNDMASK
+// One bisection level in VOP3 with the borrow as the select: b = (k < c) from
+// v_sub_co_u32's borrow, k = b ? k : k - c and off = b ? 0 : S by two
+// v_cndmask_b32_e64, where min(k, k - c) cost a v_min_u32 (a slow
+// instruction, ~6.5 cycles at the margin in this loop; a v_cndmask_b32_e64
+// among v_bitop3_b32 costs ~2.7: tools/diag/valu_rate7.cpp).  The s_nop gives
+// the two wait states a VALU-written SGPR needs before a VALU reads it (hipcc
+// puts one instruction and an s_nop 0 there).  W: w = b ? w_lo : w_hi (the
+// 32-bit level's word select), else unused.
+template <int S, bool W>
+__device__ __forceinline__ void kth_level(u32& k, u32 c, u32& off, u32& w, u32 w_hi) {
+    u32 d, k2, o, w2;
+    u64 b;
+    if (W)
+        asm("v_sub_co_u32_e64 %0, %4, %5, %6\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %1, %0, %5, %4\n\t"
+            "v_cndmask_b32_e64 %2, %7, 0, %4\n\t"
+            "v_cndmask_b32_e64 %3, %9, %8, %4"
+            : "=&v"(d), "=&v"(k2), "=&v"(o), "=v"(w2), "=&s"(b)
+            : "v"(k), "v"(c), "i"(S), "v"(w), "v"(w_hi));
+    else
+        asm("v_sub_co_u32_e64 %0, %3, %4, %5\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %1, %0, %4, %3\n\t"
+            "v_cndmask_b32_e64 %2, %6, 0, %3"
+            : "=&v"(d), "=&v"(k2), "=v"(o), "=&s"(b)
+            : "v"(k), "v"(c), "i"(S));
+    k = k2;
+    off = o;
+    if (W) w = w2;
+}
+__device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
+    u32 w = (u32)x, b32, s16, s8;
+    kth_level<32, true>(k, c_lo, b32, w, (u32)(x >> 32));
+    kth_level<16, false>(k, __popc(w & 0xFFFFu), s16, w, 0u);
+    w >>= s16;
+    kth_level<8, false>(k, __popc(w & 0xFFu), s8, w, 0u);
+    const u32 byte = __builtin_amdgcn_ubfe(w, s8, 8);
+    // the disjoint level offsets ORed by one v_bitop3_b32 (hipcc's v_or3_b32 is slow)
+    const u32 lvl = (u32)__builtin_amdgcn_bitop3_b32(b32, s16, s8, 0xFE);
+    return add_lshl3(lvl, tab[byte * 8u + k]);
+}
+#else
 __device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
     const u32 lo = (u32)x, hi = (u32)(x >> 32);
     const bool up = k >= c_lo;
@@ -433,6 +483,7 @@ __device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t
     const u32 byte = __builtin_amdgcn_ubfe(w, s8, 8);
     return add_lshl3(b32 | s16 | s8, tab[byte * 8u + k]);
 }
+#endif
 __device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
     return kth_bit_off(x, k, c_lo, tab) >> 3;
 }

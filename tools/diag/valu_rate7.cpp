@@ -12,6 +12,17 @@
 #define SA "v_lshl_add_u64 v[56:57], v[42:43], 1, v[40:41]\n"
 #define SR "v_bfrev_b32_e32 v58, v44\n"
 #define SC "v_bcnt_u32_b32 v58, v44, 0\n"
+#define SR6 "v_bfrev_b32_e64 v58, v44\n"
+#define SL32 "v_lshrrev_b32_e64 v58, 4, v44\n"
+#define SCN "v_cndmask_b32_e64 v58, v44, v45, s[0:1]\n"
+#define SMN "v_min_u32_e64 v58, v44, v45\n"
+#define D1 "v_add_u32_e64 v60, v45, v46\n"
+#define SL2 "v_lshrrev_b32_e64 v59, 4, v47\n"
+#define SL32E "v_lshrrev_b32_e32 v58, 4, v44\n"
+#define SCNE "v_cndmask_b32_e32 v58, v44, v45, vcc\n"
+#define SCNT "v_bcnt_u32_b32 v58, v44, 0\n"
+#define SAB "v_alignbit_b32 v58, v44, v45, 4\n"
+#define SMAD "v_mul_hi_u32 v58, v44, v45\n"
 #define A1 "v_and_b32_e32 v60, v45, v46\n"
 #define A2 "v_and_b32_e32 v61, v49, v50\n"
 #define A3 "v_and_b32_e32 v62, v53, v54\n"
@@ -28,8 +39,9 @@
 #define C2 "v_bitop3_b32 v61, v49, v50, v50 bitop3:0xc0\n"
 #define C3 "v_bitop3_b32 v62, v53, v54, v54 bitop3:0xc0\n"
 #define X8(a) a a a a a a a a
+#define X4(a) a a a a
 #define CLOB "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", \
-             "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63"
+             "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "s0", "s1"
 template <int OP>
 __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed) {
     asm volatile(
@@ -56,6 +68,27 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed) {
         if (OP == 14) asm volatile(X8(C1 C2 C3 C1) ::: CLOB);
         if (OP == 15) asm volatile(X8(S S A1 A2) ::: CLOB);
         if (OP == 16) asm volatile(X8(S S C1 C2) ::: CLOB);
+        if (OP == 17) asm volatile(X8(SR6 C1 C2 C3) ::: CLOB);
+        if (OP == 18) asm volatile(X8(SL32 C1 C2 C3) ::: CLOB);
+        if (OP == 19) asm volatile(X8(SCN C1 C2 C3) ::: CLOB);
+        if (OP == 20) asm volatile(X8(SMN C1 C2 C3) ::: CLOB);
+        if (OP == 21) asm volatile(X8(S D1 C2 C3) ::: CLOB);
+        if (OP == 22) asm volatile(X8(S C1 S C2) ::: CLOB);
+        if (OP == 23) asm volatile(X4(S C1 C2 C3 C1 C2 C3 C1) ::: CLOB);
+        if (OP == 24) asm volatile(X8(S SR6 C1 C2) ::: CLOB);
+        if (OP == 25) asm volatile(X8(SR6 SR6 C1 C2) ::: CLOB);
+        if (OP == 26) asm volatile(X8(SR6 SR6 SR6 SR6) ::: CLOB);
+        if (OP == 27) asm volatile(X8(SL32 SL2 SL32 SL2) ::: CLOB);
+        if (OP == 28) asm volatile(X8(SL32E SL32E SL32E SL32E) ::: CLOB);
+        if (OP == 29) asm volatile(X8(SCN SCN SCN SCN) ::: CLOB);
+        if (OP == 30) asm volatile(X8(SCNE SCNE SCNE SCNE) ::: CLOB);
+        if (OP == 31) asm volatile(X8(SL32 C1 SL2 C2) ::: CLOB);
+        if (OP == 32) asm volatile(X8(S SL32 SL2 C1) ::: CLOB);
+        if (OP == 33) asm volatile(X8(S SL32 S SL2) ::: CLOB);
+        if (OP == 34) asm volatile(X8(SL32E C1 C2 C3) ::: CLOB);
+        if (OP == 35) asm volatile(X8(SAB C1 C2 C3) ::: CLOB);
+        if (OP == 36) asm volatile(X8(SMAD C1 C2 C3) ::: CLOB);
+        if (OP == 37) asm volatile(X8(SCNT SCNT SCNT SCNT) ::: CLOB);
     }
     unsigned r;
     asm volatile("v_mov_b32 %0, v56" : "=v"(r)::CLOB);
@@ -86,7 +119,7 @@ int main() {
     unsigned* out;
     (void)hipMalloc(&out, (size_t)8192 * 256 * 4);
     for (int i = 0; i < 3; i++) run<0>(out, 2048);
-    for (int b : {1024, 2048}) {
+    for (int b : {2048}) {
         printf("-- %d waves/SIMD\n", b / 256);
         report<0>(out, "8 x (shl64, and_e32 x3)", b);
         report<1>(out, "8 x (shl64, and_e64 x3)", b);
@@ -105,6 +138,27 @@ int main() {
         report<14>(out, "32 bitop3 and", b);
         report<15>(out, "8 x (shl64 x2, and_e32 x2)", b);
         report<16>(out, "8 x (shl64 x2, bitop3 and x2)", b);
+        report<17>(out, "8 x (bfrev_e64, bitop3 and x3)", b);
+        report<18>(out, "8 x (lshrrev_b32_e64, bitop3 and x3)", b);
+        report<19>(out, "8 x (cndmask_e64, bitop3 and x3)", b);
+        report<20>(out, "8 x (min_u32_e64, bitop3 and x3)", b);
+        report<21>(out, "8 x (shl64, add_u32_e64, bitop3 x2)", b);
+        report<22>(out, "16 x (shl64, bitop3)", b);
+        report<23>(out, "4 x (shl64, bitop3 x7)", b);
+        report<24>(out, "8 x (shl64, bfrev_e64, bitop3 x2)", b);
+        report<25>(out, "8 x (bfrev_e64 x2, bitop3 x2)", b);
+        report<26>(out, "32 bfrev_e64", b);
+        report<27>(out, "32 lshrrev_b32_e64", b);
+        report<28>(out, "32 lshrrev_b32_e32", b);
+        report<29>(out, "32 cndmask_e64 (sgpr mask)", b);
+        report<30>(out, "32 cndmask_e32 (vcc)", b);
+        report<31>(out, "16 x (lshrrev_b32_e64, bitop3)", b);
+        report<32>(out, "8 x (shl64, lshrrev_e64 x2, bitop3)", b);
+        report<33>(out, "16 x (shl64, lshrrev_e64)", b);
+        report<34>(out, "8 x (lshrrev_b32_e32, bitop3 x3)", b);
+        report<35>(out, "8 x (alignbit, bitop3 x3)", b);
+        report<36>(out, "8 x (mul_hi_u32, bitop3 x3)", b);
+        report<37>(out, "32 bcnt", b);
     }
     return 0;
 }

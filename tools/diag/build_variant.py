@@ -20,7 +20,8 @@ def main():
     inc = ["-I", os.path.join(ROOT, "include")]
     with tempfile.TemporaryDirectory() as tmp:
         j = lambda f: os.path.join(tmp, f)  # noqa: E731
-        subprocess.check_call([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", *inc, "--cuda-device-only", "-S",
+        subprocess.check_call([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-pragma-unroll-threshold=200000", *inc,
+                               "--cuda-device-only", "-S",
                                "-o", j("o.s"), src], stderr=subprocess.DEVNULL)
         subprocess.check_call([sys.executable, rewrite, j("o.s"), j("b.s"), *rargs])
         subprocess.check_call([os.path.join(llvm, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa",

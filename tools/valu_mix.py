@@ -82,7 +82,8 @@ KERNELS = {"rollout_kernel<0, false>": "rollout_kernelILi0ELb0ELb0E", "rollout_k
 
 def compile_asm():
     out = os.path.join(tempfile.mkdtemp(), "othello.s")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-x", "hip", "--cuda-device-only", "-S",
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-mllvm", "-pragma-unroll-threshold=200000",
+                    "-x", "hip", "--cuda-device-only", "-S",
                     "-o", out, os.path.join(ROOT, "subproc_amd", "csrc", "othello.hip"),
                     "-I", os.path.join(ROOT, "include")], check=True, capture_output=True)
     return out

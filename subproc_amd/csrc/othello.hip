@@ -119,7 +119,9 @@ __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq,
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
-    const int v = eval_linear(w, P2, moves<879>(P2, O2));  // |v| < 2^14 (fill order: bitboard.hpp analyse)
+    // |v| < 2^14; fill order 7-9-8 (bitboard.hpp analyse): 9 same-bank v_bitop3_b32 in
+    // this child loop against 13 at 8-7-9, +2-4% eval env-steps/s (tools/diag/r03_evalorder.sh)
+    const int v = eval_linear(w, P2, moves<798>(P2, O2));
     return ((u32)((1 << 20) - v) << 6) | sq;
 }
 

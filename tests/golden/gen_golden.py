@@ -19,7 +19,8 @@ board.py's own ``puttables`` / ``put_s`` / ``is_game_over`` so the fixtures pin
 (board, move) -> next state semantics to the reference, and the RNG spec to a
 second independent implementation.
 
-Usage:  python tests/golden/gen_golden.py        (≈1–2 min on 8 cores)
+Usage:  python tests/golden/gen_golden.py [--out DIR]   (all 24 fixtures, ≈1–2 min on 8 cores)
+        python tests/golden/gen_golden.py --only batch_stats|td_records|runner|board_api
 """
 import json
 import random
@@ -731,36 +732,11 @@ def main():
 
     # ---------------------------------------------------------------- TD state map (§8f row 2)
     # ProgressPositionMovesLearn.__update_state_for_a_book / __update_state_map
-    # (progress_position_moves_learn.py:37-62) over the 256 rollout_random games as
+    # (progress_position_moves_learn.py:37-62) run from the reference module
+    # itself (reference_state_map) over the 256 rollout_random games as
     # learn_books hands them over (replearn.py:34-39: records sorted by turn,
-    # reversed).  The key is the reference's own hash_from_book and the terminal
-    # value uses its board_from_a_book; the module itself imports pyres/slack
-    # (absent), so only the five EMA lines are restated here.
-    param = ns["ProgressPositionMovesParameter"]()
-    bfab = ns["board_from_a_book"]
-    a_, l_ = 0.03, 0.90  # ProgressPositionMovesLearn.__init__ (22-24)
-    store = {}
-    for g in range(len(z["plies"])):
-        b = from_bits(ib, iw, Black)
-        recs = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
-                 "end": b.is_game_over()}]
-        for code in z["moves"][g]:
-            if code == 255:
-                break
-            assert b.put_s(code_to_str(b, int(code))) >= 0
-            recs.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
-                         "end": b.is_game_over()})
-        book = list(reversed(sorted(recs, key=lambda x: int(x["turn"]))))
-        last_turn = int(book[0]["turn"])
-        last_board = bfab(book[0])
-        vb = last_board.n_black() - last_board.n_white()
-        vw = last_board.n_white() - last_board.n_black()
-        for rec in book:
-            for side, value in (("O", vb), ("X", vw)):
-                key = param.hash_from_book(rec, side)
-                cur = float(store.get(key, 0))
-                new = float(value) * (l_ ** (last_turn - int(rec["turn"])))
-                store[key] = new if cur == 0 else cur * (1 - a_) + new * a_
+    # reversed).
+    store = reference_state_map([game_book_learn_order(z, g) for g in range(len(z["plies"]))])
     ks = sorted(store)
     np.savez_compressed(os.path.join(OUT, "td_state.npz"), source=np.array("rollout_random"),
                         games=np.array(len(z["plies"])), hash=np.array(ks), value=np.array([store[k] for k in ks]),
@@ -808,6 +784,125 @@ def load_reference_learn_base():
     return ns, mod_slack
 
 
+def load_reference_learner():
+    """progress_position_moves_learn.py exec'd as the reference wrote it, with
+    its Python 2 print statements (lines 38, 123, 155, 156, 168, 173, 221, 222)
+    turned into print(...) calls in memory, and its imports served by:
+      * board, parameter, parameter_progress_position_moves_learn, learn_base:
+        the reference's own modules, exec'd as above (board.py through its shim);
+      * slack: a stub that records the text (no network);
+      * pyres, parallel_learner_task, config, replearn: stubs -- they are only
+        reached from the Resque fan-out (__fit_parameters, 115-158) and
+        configure(), which the state-map update does not touch.
+    sklearn and numpy are the real packages.  Nothing is written to
+    /root/reference and no source is copied."""
+    import re
+    import types
+    src = open("/root/reference/progress_position_moves_learn.py").read().split("\n")
+    print_lines = [i for i, ln in enumerate(src) if re.match(r"\s*print ", ln)]
+    assert [i + 1 for i in print_lines] == [38, 123, 155, 156, 168, 173, 221, 222], \
+        "progress_position_moves_learn.py changed; the print shim no longer applies"
+    for i in print_lines:
+        m = re.match(r"(\s*)print (.*?)(\s*#.*)?$", src[i])
+        src[i] = "%sprint(%s)%s" % (m.group(1), m.group(2), m.group(3) or "")
+    lb_ns, slack = load_reference_learn_base()
+    ppml = load_reference_counts(want_ns=True)
+
+    def module(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        return m
+
+    class ResQ:  # pyres: never reached by the state-map update
+        def __init__(self, *a, **k):
+            raise RuntimeError("pyres stub: the Resque fan-out is out of scope")
+
+    mods = {
+        "board": module("board", **RB),
+        "slack": slack,
+        "learn_base": module("learn_base", **lb_ns),
+        "parameter": module("parameter", board_from_a_book=ppml["board_from_a_book"]),
+        "parameter_progress_position_moves_learn": module("parameter_progress_position_moves_learn", **ppml),
+        "pyres": module("pyres", ResQ=ResQ),
+        "parallel_learner_task": module("parallel_learner_task", ParallelLearnerTask=object),
+        "config": module("config", redis_hostname_port_from_config=lambda c: None),
+        "replearn": module("replearn", get_instance_from_config=None),
+    }
+    saved = {k: sys.modules.get(k) for k in mods}
+    sys.modules.update(mods)
+    try:
+        ns = {"__name__": "reference_progress_position_moves_learn"}
+        exec(compile("\n".join(src), "reference_progress_position_moves_learn.py", "exec"), ns)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return ns, ppml
+
+
+class RedisLikeStore:
+    """The parameter store as RedisParameterStore presents it to the learner
+    (redis_parameter_store.py:26-39): values go in as redis-py encodes them
+    (repr() of a float, str() of an int) and come back as strings, so float()
+    reads back exactly the value set."""
+
+    def __init__(self):
+        self.kv = {}
+
+    def exists(self, key):
+        return ":".join(key) in self.kv
+
+    def get(self, key):
+        return self.kv.get(":".join(key))
+
+    def set(self, key, value):
+        self.kv[":".join(key)] = repr(value) if isinstance(value, float) else str(value)
+        return True
+
+
+def reference_state_map(books):
+    """{hash: value} after ProgressPositionMovesLearn.__update_state_for_a_book
+    (progress_position_moves_learn.py:37-48) -> __update_state_map (50-62), the
+    reference's own code, over `books` in order (learn_and_update_batch, 88-91).
+    The learner's print of each terminal record (line 38) is discarded."""
+    import contextlib
+    import io
+    ns, ppml = load_reference_learner()
+    store = RedisLikeStore()
+
+    class Learner(ns["ProgressPositionMovesLearn"]):
+        def _param_store(self):
+            return store
+
+    lrn = Learner()
+    lrn.parameter = ppml["ProgressPositionMovesParameter"]()  # what configure() instantiates
+    update = lrn._ProgressPositionMovesLearn__update_state_for_a_book
+    with contextlib.redirect_stdout(io.StringIO()):
+        for i, book in enumerate(books):
+            update(i, book)
+    prefix = "param:state:"
+    assert all(k.startswith(prefix) for k in store.kv)
+    return {k[len(prefix):]: float(v) for k, v in store.kv.items()}
+
+
+def game_book_learn_order(z, g):
+    """Game g of a rollout fixture as the recorder writes it (the record after
+    Board() and after every put_s, game_runner.py:169-184) and learn_books hands
+    it to the learner: sorted by turn, reversed (replearn.py:34-39)."""
+    ib, iw = to_bits(Board())
+    b = from_bits(ib, iw, Black)
+    recs = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn, "end": b.is_game_over()}]
+    for code in z["moves"][g]:
+        if code == 255:
+            break
+        assert b.put_s(code_to_str(b, int(code))) >= 0
+        recs.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
+                     "end": b.is_game_over()})
+    return list(reversed(sorted(recs, key=lambda x: int(x["turn"]))))
+
+
 def replay_terminal(sb, sw, st, moves):
     """The terminal record a game's recorder writes (game_recorder.py:107-114):
     the board after the recorded move codes, driven through board.py's put_s."""
@@ -828,7 +923,7 @@ def batch_stats_fixtures():
     import fnmatch
     import subprocess
     if os.environ.get("PYTHONHASHSEED") != "0":
-        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--only", "batch_stats"],
+        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--only", "batch_stats", "--out", OUT],
                               env=dict(os.environ, PYTHONHASHSEED="0"))
         return
     ns, slack = load_reference_learn_base()
@@ -931,37 +1026,17 @@ def td_records_fixtures():
     """The learner's state-map update over books that are not clean GameRunner
     games (books read from any store: td.StateMap.update_from_records).
     __update_state_for_a_book / __update_state_map
-    (progress_position_moves_learn.py:37-62) over each book in the given order:
-    the key is the reference's own hash_from_book, the terminal value its
-    board_from_a_book (both exec'd against the shimmed board.py), and the five
-    EMA lines are restated as for td_state.npz (the module imports pyres and
-    slack).  Books are built from rollout_random.npz games replayed through
+    (progress_position_moves_learn.py:37-62) over each book in the given order,
+    run from the reference module itself (reference_state_map).  Books are built from rollout_random.npz games replayed through
     board.py, then altered: records dropped (gaps in turn), repeated, shuffled
     after the terminal, turns as strings, board strings cut short (the rest of
     the squares stay the opening's) or holding other characters ('o', 'x',
     '.', ...: Empty), and boards of random characters."""
-    ns = load_reference_counts(want_ns=True)
-    param = ns["ProgressPositionMovesParameter"]()
-    bfab = ns["board_from_a_book"]
-    a_, l_ = 0.03, 0.90  # ProgressPositionMovesLearn.__init__ (22-24)
     z = np.load(os.path.join(OUT, "rollout_random.npz"))
-    ib, iw = to_bits(Board())
-
-    def game_book(g):
-        b = from_bits(ib, iw, Black)
-        recs = [{"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn, "end": b.is_game_over()}]
-        for code in z["moves"][g]:
-            if code == 255:
-                break
-            assert b.put_s(code_to_str(b, int(code))) >= 0
-            recs.append({"book": b.serialize_board(), "whosturn": b.serialize_turn(), "turn": b.nturn,
-                         "end": b.is_game_over()})
-        return list(reversed(sorted(recs, key=lambda x: int(x["turn"]))))  # learn_books' order
-
     rnd = random.Random(20261017)
     books, kinds = [], []
     for g in range(40):
-        book = game_book(g)
+        book = game_book_learn_order(z, g)
         kind = ["clean", "gaps", "repeats", "shuffled", "str_turns", "short", "chars", "random_boards"][g % 8]
         if kind == "gaps":
             book = [book[0]] + [r for r in book[1:] if rnd.random() < 0.6]
@@ -982,27 +1057,20 @@ def td_records_fixtures():
             book = [dict(r, book="".join(rnd.choice("OX-OX-ox.") for _ in range(64))) for r in book]
         books.append(book)
         kinds.append(kind)
-    store = {}
-    for book in books:  # learn_and_update_batch (94-96) -> __update_state_for_a_book (37-48)
-        last_turn = int(book[0]["turn"])
-        last_board = bfab(book[0])
-        vb = last_board.n_black() - last_board.n_white()
-        vw = last_board.n_white() - last_board.n_black()
-        for rec in book:
-            for side, value in (("O", vb), ("X", vw)):
-                key = param.hash_from_book(rec, side)
-                cur = float(store.get(key, 0))
-                new = float(value) * (l_ ** (last_turn - int(rec["turn"])))
-                store[key] = new if cur == 0 else cur * (1 - a_) + new * a_
+    # learn_and_update_batch (88-91) -> __update_state_for_a_book (37-48), run from the reference
+    store = reference_state_map(books)
     ks = sorted(store)
-    out = {"source": "progress_position_moves_learn.py:37-62 over rollout_random.npz games replayed through "
-                     "board.py and altered; hash_from_book / board_from_a_book exec'd from the reference",
+    out = {"source": "progress_position_moves_learn.py:37-62 exec'd from the reference (reference_state_map) over "
+                     "rollout_random.npz games replayed through board.py and altered",
            "kinds": kinds, "books": books, "hash": ks, "value": [store[k] for k in ks]}
     json.dump(out, open(os.path.join(OUT, "td_records.json"), "w"))
     print("td_records.json:", len(books), "books,", sum(map(len, books)), "records,", len(ks), "keys")
 
 
 if __name__ == "__main__":
+    if "--out" in sys.argv:  # another directory (tests/test_golden_regen.py regenerates into a temp dir)
+        OUT = os.path.abspath(sys.argv[sys.argv.index("--out") + 1])
+        os.makedirs(OUT, exist_ok=True)
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     if only == "batch_stats":
         batch_stats_fixtures()
@@ -1012,4 +1080,7 @@ if __name__ == "__main__":
         runner_fixtures(mp.Pool(8))
         print("runner fixtures written to", OUT)
     else:
+        # every fixture: main() writes the rollouts the last two read
         main()
+        batch_stats_fixtures()
+        td_records_fixtures()

@@ -39,34 +39,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md
-# VALU issue: a wave64 instruction can issue every 2 cycles on a SIMD-32
-# (MI355X_MICROARCH.md), 1024 SIMDs at the 2.4 GHz max clock.  Measured on the
-# box (tools/diag/valu_rate*.cpp) only plain VOP2 logic reaches that (~2.2
-# cycles); the 64-bit shifts, bfi, bcnt, cndmask ... these kernels are made of
-# take ~4.  The ceiling priced for a kernel is therefore its hot loop's
-# mix-weighted mean (tools/valu_mix.py -> profiles/valu_mix.json).
+# VALU issue peak: a wave64 instruction can issue every 2 cycles on a SIMD-32
+# (MI355X_MICROARCH.md), 1024 SIMDs at the 2.4 GHz max clock = 1.229e12
+# wave-instructions/s.  valu.frac is the fraction of THIS hardware figure.
+# Measured on the box (tools/diag/valu_rate*.cpp) only plain logic streams at
+# ~2.2 cycles; 64-bit shifts, bfrev, bcnt ... take ~4, so these kernels cannot
+# reach it: the ceilings priced from each hot loop's own instruction mix
+# (tools/valu_mix.py -> profiles/valu_mix.json) are reported beside it under
+# valu.model, as model statements, not as the roofline.
 VALU_PEAK_HW = 1024 * 2.4e9 / 2
 
 
 def valu_entry(kernel, achieved, **extra):
-    """VALU roofline of `kernel` at `achieved` wave-instructions/s."""
-    peak, mix = VALU_PEAK_HW, None
+    """VALU roofline of `kernel` at `achieved` wave-instructions/s: the fraction
+    of the hardware issue peak, with the mix-model ceilings under 'model'."""
+    e = {"achieved": achieved, "peak": VALU_PEAK_HW, "unit": "wave-instr/s", "frac": achieved / VALU_PEAK_HW,
+         "peak_basis": "2 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz (MI355X_MICROARCH.md)"}
+    mix = None
     try:
         with open(os.path.join(ROOT, "profiles", "valu_mix.json")) as f:
             mix = json.load(f)["kernels"].get(kernel)
     except (OSError, ValueError, KeyError):
         pass
     if mix:
-        peak = mix["peak_winstr_s"]
-    e = {"achieved": achieved, "peak": peak, "unit": "wave-instr/s", "frac": achieved / peak,
-         "peak_basis": ("hot-loop mix, %.2f cycles/instr (profiles/valu_mix.json)" % mix["mean_cycles"]) if mix
-         else "2 cycles/instr (SIMD-32 issue)",
-         "frac_of_2cycle_issue": achieved / VALU_PEAK_HW}
-    if mix and "peak_winstr_s_mixed" in mix:
-        # the same loop priced with the in-mix costs (tools/valu_mix.py mean_cycles_mixed:
-        # a slow VOP3 instruction makes the fast ones after it cost ~2.95 / ~3.7)
-        e["peak_mixed"] = mix["peak_winstr_s_mixed"]
-        e["frac_mixed"] = achieved / mix["peak_winstr_s_mixed"]
+        m = {"basis": "ceilings fitted to the hot loop's static instruction mix with per-opcode costs measured "
+                      "on the box (tools/valu_mix.py); a model, not a hardware peak",
+             "mean_cycles": mix["mean_cycles"], "peak": mix["peak_winstr_s"], "frac": achieved / mix["peak_winstr_s"]}
+        if "peak_winstr_s_mixed" in mix:
+            m.update(mean_cycles_mixed=mix.get("mean_cycles_mixed"), peak_mixed=mix["peak_winstr_s_mixed"],
+                     frac_mixed=achieved / mix["peak_winstr_s_mixed"])
+        e["model"] = m
     e.update(extra)
     return e
 
@@ -82,14 +84,24 @@ ROLLOUT_BYTES_PER_GAME = 18  # final board 16 + diff 1 + plies 1 written; openin
 
 def load_profile():
     """Per-launch PMC figures of the newest committed round profile
-    (profiles/rNN_profile_summary.json, made by tools/profile_round.sh)."""
+    (profiles/rNN_profile_summary.json, made by tools/profile_round.sh), if it
+    was measured on the library this run loads: returns (file, kernels, stale)
+    where stale describes a profile of another build (its PMC figures are then
+    not used: no line mixes the counters of one build with the clock of another)."""
     import glob
+
+    from subproc_amd._lib import library_sha16
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_profile_summary.json")))
     if not files:
-        return None, {}
+        return None, {}, None
     with open(files[-1]) as f:
-        return os.path.basename(files[-1]), json.load(f).get("kernels", {})
+        d = json.load(f)
+    name, have = os.path.basename(files[-1]), library_sha16()
+    if d.get("library_sha16") != have:
+        return name, {}, {"profile": name, "profile_library_sha16": d.get("library_sha16"),
+                          "library_sha16": have, "note": "profile of another build: PMC figures omitted"}
+    return name, d.get("kernels", {}), None
 
 
 def profile_entry(kernels, name, grid=None, largest=False):
@@ -207,6 +219,8 @@ def main():
                         "unit": r["unit"], "ms_per_step": r["ms_per_step"], "launch_ms": r["roofline"]["launch_ms"],
                         "valu_frac": r.get("valu", {}).get("frac")}
             guarded("rollout_1stream", serial)
+        if args.workload in ("rollout", "greedy") and "rollout_sharded" not in skip:
+            guarded("rollout_sharded_steps10", lambda: _bench_sharded(torch, args, policy))
         if args.workload == "rollout" and "rollout_16M" not in skip:
             guarded("rollout_16M", lambda: _bench_rollout_big(ops, torch, dev, args))
         def policy_line(pol):
@@ -240,6 +254,9 @@ def main():
             "step_65536": _bench_step(ops, torch, dev, stream, args, 65536, world, barrier, max_over_ranks,
                                       launches=200, index0=rank * 65536)}
     if rank == 0:
+        from subproc_amd._lib import library_sha16
+
+        out["library_sha16"] = library_sha16()  # the build measured (profiles/ digests carry theirs)
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.destroy_process_group()
@@ -399,7 +416,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     # roofline: algorithmic bytes of one launch / that launch's duration (events on its stream)
     achieved = n * ROLLOUT_BYTES_PER_GAME / (launch_ms * 1e-3) / 1e9
     kname = "rollout_kernel<%d, false>" % pid
-    pfile, kernels = load_profile()
+    pfile, kernels, stale = load_profile()
     prof = profile_entry(kernels, kname, largest=True) if n == 1 << 20 else None
     # "bound" prices the launch's algorithmic HBM bytes (the contract's roofline);
     # the resource that binds this kernel is VALU issue ("binding", and "valu")
@@ -407,7 +424,7 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
                        "frac": achieved / HBM_PEAK_GBS,
                        "traffic": prof.get("hbm_bytes") if prof else None,
                        "kernel": kname, "launch_ms": launch_ms, "launch_ms_median": median_ms,
-                       "step_ms": step_ms, "profile": pfile if prof else None,
+                       "step_ms": step_ms, "profile": pfile if prof else None, "profile_stale": stale,
                        "note": "%d algorithmic B/game written (final board, diff, plies); the kernel is "
                                "integer-VALU-bound, see 'valu'. launch_ms: one launch's duration; step_ms: "
                                "stream time per step with %d launches in flight" % (ROLLOUT_BYTES_PER_GAME,
@@ -472,13 +489,13 @@ def _bench_step(ops, torch, dev, stream, args, n, world, barrier, max_over_ranks
     kern_ms = ev0.elapsed_time(ev1) / K
     steps = n * K * world
     achieved = n * STEP_BYTES / (kern_ms * 1e-3) / 1e9
-    pfile, kernels = load_profile()
+    pfile, kernels, stale = load_profile()
     prof = profile_entry(kernels, "step_kernel", n)
     r = {"metric": "env-steps/sec (batched step)", "value": steps / elapsed, "unit": "env-steps/s",
          "n_gpus": world, "batch": n, "launches": K, "us_per_launch": kern_ms * 1e3, "dtype": "u64",
          "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("hbm_bytes") if prof else None,
-                      "kernel": "step_kernel", "profile": pfile if prof else None}}
+                      "kernel": "step_kernel", "profile": pfile if prof else None, "profile_stale": stale}}
     if prof and "SQ_INSTS_VALU" in prof:
         va = prof["SQ_INSTS_VALU"] / (kern_ms * 1e-3)
         r["valu"] = valu_entry("step_kernel", va)
@@ -512,6 +529,29 @@ def _bench_step_graph(ops, torch, dev, args, n=65536, launches=200):
     return {"metric": "env-steps/sec (batched step, HIP graph of %d launches)" % launches,
             "value": n * launches / dt, "unit": "env-steps/s", "batch": n, "launches": launches,
             "us_per_launch": dt / launches * 1e6}
+
+
+def _bench_sharded(torch, args, policy, steps=10, reps=3):
+    """The product's multi-GPU entry as a single-process caller uses it:
+    dist.rollout_sharded(steps * games, steps=steps) -- `steps` launches of
+    `games` games pipelined on two streams (ops.rollout_batches) -- timed by
+    the host clock around the call and a device sync (median of `reps`)."""
+    from subproc_amd.dist import rollout_sharded
+
+    n = args.games
+    rollout_sharded(2 * n, args.seed, policy, steps=2, game_id_base=1 << 45)  # first-use warm-up
+    torch.cuda.synchronize()
+    rates = []
+    for r in range(reps):
+        t0 = time.perf_counter()
+        hist, _ = rollout_sharded(steps * n, args.seed, policy, steps=steps, game_id_base=(1 << 45) + (r + 1) * steps * n)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rates.append(int(hist[132]) / dt)
+    rates.sort()
+    return {"metric": "env-steps/sec (dist.rollout_sharded, %d pipelined launches of %d games, one process)"
+                      % (steps, n), "value": rates[len(rates) // 2], "unit": "env-steps/s", "reps": rates,
+            "policy": policy}
 
 
 def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):

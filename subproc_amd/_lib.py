@@ -101,3 +101,13 @@ def check(status, what):
 
 def version():
     return load().oth_version().decode()
+
+
+def library_sha16(path=None):
+    """First 16 hex digits of the SHA-256 of the HIP library file: the build
+    identity that bench lines and profile digests are stamped with (the build
+    is deterministic: the same sources and flags give the same file)."""
+    import hashlib
+
+    with open(path or LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]

@@ -29,7 +29,7 @@ def bench_game_id0(step, rank, world, n):
 
 
 def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None, rollout_fn=None, device=None,
-                    game_id_base=0):
+                    game_id_base=0, steps=1, streams=2):
     """Play `total_games` games split over the ranks of `group`; returns
     (global histogram int64[133] on every rank, local game count).
 
@@ -37,25 +37,39 @@ def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None,
     reduced histogram is identical for any world size (bit-exact check of the
     all-reduce path: tests/test_dist.py).  `rollout_fn(n, seed, game_id0,
     policy, n_random, hist)` defaults to the HIP kernel (subproc_amd.ops.rollout).
+
+    steps > 1 splits the rank's range into `steps` consecutive launches
+    pipelined over `streams` HIP streams (ops.rollout_batches: the repeated
+    launches of bench.py's timed loop); the histogram is the same.  With a
+    custom `rollout_fn` the chunks are played one call each, in order.
     """
+    if steps < 1:
+        raise ValueError("steps must be >= 1")
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     begin, end = shard_range(total_games, rank, world)
-    if rollout_fn is None:
-        from . import ops
-
-        def rollout_fn(n, seed, game_id0, policy, n_random, hist):
-            ops.rollout(n, seed, game_id0, policy, n_random, hist=hist, device=hist.device, want_boards=False,
-                        want_diff=False, want_plies=False)
-
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
+    if rollout_fn is None and device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=device)
-    if end > begin:
-        rollout_fn(end - begin, seed, game_id_base + begin, policy, n_random, hist)
+    local = end - begin
+    if local > 0:
+        if rollout_fn is None:
+            from . import ops
+            per, rest = divmod(local, steps)
+            if per:  # `steps` equal launches, then the remainder
+                ops.rollout_batches(per, steps, seed, game_id_base + begin, policy, n_random, hist=hist, device=device,
+                                    streams=streams)
+            if rest:
+                ops.rollout(rest, seed, game_id_base + begin + per * steps, policy, n_random, hist=hist,
+                            device=device, want_boards=False, want_diff=False, want_plies=False)
+        else:
+            for c in range(steps):
+                b, e = shard_range(local, c, steps)
+                if e > b:
+                    rollout_fn(e - b, seed, game_id_base + begin + b, policy, n_random, hist)
     if world > 1:
         reduce_histogram(hist, group)
-    return hist, end - begin
+    return hist, local
 
 
 def reduce_histogram(hist, group=None):

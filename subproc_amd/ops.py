@@ -262,6 +262,92 @@ def rollout(n, seed, game_id0=0, policy="random", n_random=10, start=None, start
     return RolloutResult(fb, df, pl, mv, hist)
 
 
+_SIDE = {}
+
+
+def _side_streams(d, k):
+    """k side streams of device d, created once and reused (rollout_batches)."""
+    have = _SIDE.setdefault(d.index, [])
+    while len(have) < k:
+        have.append(torch.cuda.Stream(d))
+    return have[:k]
+
+
+def rollout_batches(n, steps, seed, game_id0=0, policy="random", n_random=10, hist=None, device="cuda", streams=2,
+                    want_boards=False, want_diff=False, want_plies=False, weights=None):
+    """`steps` back-to-back rollout launches of `n` games each, pipelined:
+    launch s plays global ids [game_id0 + s*n, +n) and the launches are issued
+    round-robin on `streams` HIP streams (torch's current stream and
+    streams - 1 side streams, each with its own work word), so the last
+    batches of one launch share the CUs with the first batches of the next
+    instead of leaving them idle (batch tail).  The result
+    equals ``rollout(n * steps, seed, game_id0, ...)`` game for game: every
+    game keeps the RNG stream of its global id, and the launches add into one
+    histogram (device atomics).  Outputs, if asked for, are (n * steps, ...)
+    in game-id order.  On return the current stream is ordered after every
+    launch; nothing is synchronised with the host.
+    """
+    if policy not in _POLICIES:
+        raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
+    if steps < 1 or n < 0 or streams < 1:
+        raise ValueError("rollout_batches: steps >= 1, n >= 0 and streams >= 1")
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("rollout_batches issues on side streams: capture ops.rollout launches instead")
+    d = _device(device)
+    pid = _POLICIES[policy]
+    if pid != POLICY_EVAL and weights is not None:
+        raise ValueError("weights apply to policy 'eval' only")
+    total = n * steps
+    fb = torch.empty((total, 2), dtype=torch.int64, device=d) if want_boards else None
+    df = torch.empty(total, dtype=torch.int8, device=d) if want_diff else None
+    pl = torch.empty(total, dtype=torch.uint8, device=d) if want_plies else None
+    if hist is None:
+        hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=d)
+    ph = _dev(hist, "hist", torch.int64, (HIST_BINS,), d)
+    lib = _lib.load()
+    wp = _weights_ptr(weights) if pid == POLICY_EVAL else None
+    with torch.cuda.device(d):
+        main = torch.cuda.current_stream()
+        side = _side_streams(d, streams - 1)
+        sts = [main] + side
+        fork = torch.cuda.Event()
+        fork.record(main)
+        for st in side:
+            st.wait_event(fork)
+        # one work word per stream (0 before and after each launch on it): the
+        # streams' cached words, as ops.rollout uses them
+        works = []
+        for st in sts:
+            with torch.cuda.stream(st):
+                works.append(work_word(d))
+        for s in range(steps):
+            i = s % len(sts)
+            st, w = sts[i], works[i]
+            g0 = game_id0 + s * n
+
+            def part(t, k=1):
+                return None if t is None else t.data_ptr() + s * n * k * t.element_size()
+
+            if pid == POLICY_EVAL:
+                rc = lib.oth_rollout_eval(None, None, seed & (2**64 - 1), g0, n_random, wp, part(fb, 2), part(df),
+                                          part(pl), None, ph, w.data_ptr(), n, st.cuda_stream)
+            else:
+                rc = lib.oth_rollout(None, None, seed & (2**64 - 1), g0, pid, n_random, part(fb, 2), part(df),
+                                     part(pl), None, ph, w.data_ptr(), n, st.cuda_stream)
+            if rc != _lib.OTH_OK:  # the failed launch's word is unknown: drop it (ops.rollout does the same)
+                _WORK.pop((d.index, st.cuda_stream), None)
+            check(rc, "oth_rollout (rollout_batches step %d)" % s)
+        for st in side:  # the caller's stream waits for every launch
+            e = torch.cuda.Event()
+            e.record(st)
+            main.wait_event(e)
+        for t in (fb, df, pl, hist):
+            if t is not None:
+                for st in side:
+                    t.record_stream(st)
+    return RolloutResult(fb, df, pl, None, hist)
+
+
 RunnerResult = namedtuple("RunnerResult", "final_boards diff plies moves hist a_black")
 
 

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, total, seed, out, bench_steps=0):
+def _worker(rank, world, port, total, seed, out, bench_steps=0, steps=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if bench_steps:
@@ -38,15 +38,15 @@ def _worker(rank, world, port, total, seed, out, bench_steps=0):
         dist.all_reduce(hist, op=dist.ReduceOp.SUM)
         local = bench_steps * total
     else:
-        hist, local = rollout_sharded(total, seed, rollout_fn=_oracle_fn, device="cpu")
+        hist, local = rollout_sharded(total, seed, rollout_fn=_oracle_fn, device="cpu", steps=steps)
     out[rank] = (hist.numpy().copy(), local)
     dist.destroy_process_group()
 
 
-def _run(world, total, seed, bench_steps=0):
+def _run(world, total, seed, bench_steps=0, steps=1):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), total, seed, out, bench_steps), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), total, seed, out, bench_steps, steps), nprocs=world, join=True)
     return dict(out)
 
 
@@ -88,6 +88,17 @@ def test_world2_histogram_equals_single_process():
     assert res[0][1] + res[1][1] == total
     s = hist_summary(ref)
     assert s["games"] == total and s["black_wins"] + s["white_wins"] + s["draws"] == total
+
+
+def test_world2_pipelined_steps_equal_single_process():
+    """rollout_sharded(steps=K): each rank's shard in K consecutive launches
+    (ragged: 301 games over 2 ranks x 4 steps) == one process over the ids."""
+    total, seed = 301, 0x5EED
+    res = _run(2, total, seed, steps=4)
+    ref = oracle.rollout(total, seed, 0)["hist"]
+    for rank in (0, 1):
+        np.testing.assert_array_equal(res[rank][0], ref)
+    assert res[0][1] + res[1][1] == total
 
 
 def test_batch_stats_payload_matches_per_book_rule():

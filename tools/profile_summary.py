@@ -74,7 +74,12 @@ def main(d):
         for key, cs in pmc(os.path.join(d, sub)).items():
             for c, v in cs.items():
                 counters.setdefault(key, {})[c] = sum(v) / len(v)
-    out = {"kernels": {}}
+    # the build every figure below was measured on (bench.py compares it with
+    # the library it runs, and marks PMC figures of another build as stale)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from subproc_amd._lib import library_sha16
+    out = {"library_sha16": library_sha16(), "kernels": {}}
     for (k, grid), cs in sorted(counters.items()):
         e = {"grid_threads": grid}
         durs = trace.get((k, grid))

@@ -685,13 +685,23 @@ def _cpu_baseline(args, workload):
     pid = 0 if workload == "random" else 1
     if pid == 1:
         games = max(1000, games // 10)
-    t0 = time.perf_counter()
-    r = oracle.rollout(games, args.seed, 0, pid, 10, n_threads=threads)
-    dt = time.perf_counter() - t0
-    steps = int(r["hist"][132])
+
+    def timed_rollout(n_games, n_threads, game_id0):
+        t0 = time.perf_counter()
+        r = oracle.rollout(n_games, args.seed, game_id0, pid, 10, n_threads=n_threads)
+        dt = time.perf_counter() - t0
+        return int(r["hist"][132]), dt
+
+    steps, dt = timed_rollout(games, threads, 0)
+    # the same restatement on one thread: 1/16 of the sample, other game ids
+    g1 = max(100, games // 16)
+    steps1, dt1 = timed_rollout(g1, 1, 1 << 40)
     return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", **host,
-            "sample": "%d %s games from the opening (%d env-steps), C mailbox restatement of board.py, "
-                      "OpenMP %d threads, %.2f s wall" % (games, workload, steps, threads, dt),
+            "sample": "%d %s games from the opening (%d env-steps), C mailbox restatement of board.py "
+                      "(oracle/othello_oracle.c: board.py's 8x8 ray scan from every cell), OpenMP %d threads, "
+                      "%.2f s wall" % (games, workload, steps, threads, dt),
+            "one_thread": {"value": steps1 / dt1, "unit": "env-steps/s", "cores": 1,
+                           "sample": "%d %s games (%d env-steps), 1 thread, %.2f s" % (g1, workload, steps1, dt1)},
             "board_py_note": "board.py itself (Python) measured at ~2.9e3 env-steps/s/core in the build container "
                              "(BASELINE.md); it cannot run on the GPU box"}
 

@@ -208,7 +208,9 @@ int oth_replay(const uint64_t* start, const uint8_t* start_turn, const uint8_t* 
  * must be the exclusive prefix sum of min(plies[i], OTH_MOVES_STRIDE) + 1, so
  * the rows of all games are one contiguous range of row_off[n-1] +
  * min(plies[n-1], OTH_MOVES_STRIDE) + 1 rows (oth_book_text serialises them in
- * one call); other offsets are the caller's risk (rows may overlap). */
+ * one call).  Other offsets are the caller's risk where rows overlap; games
+ * with disjoint rows in any order are written correctly (a block whose games'
+ * rows do not form one short range writes its bytes directly). */
 int oth_replay_rows(const uint64_t* start, const uint8_t* start_turn, const uint8_t* moves, const uint8_t* plies,
                     const int64_t* row_off, uint64_t* pos_boards, uint8_t* pos_turn, uint8_t* pos_end, int64_t n,
                     void* stream);

@@ -888,13 +888,6 @@ __device__ __forceinline__ void load_move_record(const uint8_t* row, bool vec, u
     }
 }
 
-// byte q of a staged block (game q / 129 of the block) -> (turn, end)
-__device__ __forceinline__ void unstage_byte(u32 c, const uint8_t* start_turn, int64_t game, uint8_t& t, uint8_t& e) {
-    const u32 tt = c & kTurnEscape;
-    t = (uint8_t)(tt == kTurnEscape ? start_turn[game] : tt);
-    e = (uint8_t)(c >> 7);
-}
-
 // The bursts go out through a per-wave LDS exchange: after a lane has built
 // half a burst (4 rows = 64 B of one line), the wave's 64 half-lines are
 // stored by 4 lanes each, so a store instruction writes 16 half-lines of 64
@@ -933,23 +926,43 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
     const int nb = (int)min<int64_t>(kBlock, n - blk0);
     const int lane = threadIdx.x;
     const int wl = lane & 63, wbase = lane & ~63;
-    // the block's first output row, and (packed) the 16-B chunk it starts in
-    const int64_t base = PACKED ? row_off[blk0] : blk0 * OTH_POS_STRIDE;
-    const int64_t base_al = PACKED ? (base & ~(int64_t)15) : base;
-    // the block's turn / end bytes: global [base, base + bytes); with row
-    // offsets other than the prefix sum the header asks for, a block whose
-    // range would overrun the LDS stage writes its bytes directly (and a gap
-    // between games is left as the caller had it)
-    int64_t bytes;
-    if (PACKED) {
-        const int64_t last = blk0 + nb - 1;
-        bytes = row_off[last] + min<int>(plies[last], OTH_MOVES_STRIDE) + 1 - base;
-    } else {
-        bytes = (int64_t)nb * OTH_POS_STRIDE;
+    // the block's output rows [base, base + bytes) and (packed) the 16-B chunk
+    // they start in.  Packed: the lowest first row and the highest end over the
+    // block's games (the first game's row and the last game's end for the
+    // prefix-sum offsets the header asks for).  With other offsets a block
+    // whose rows do not fit the LDS stage writes its bytes directly (and a gap
+    // between games is left as the caller had it); taken over every game, not
+    // only the last, no game's stage pointer can leave the stage.
+    int64_t base = blk0 * OTH_POS_STRIDE, bytes = (int64_t)nb * OTH_POS_STRIDE;
+    if (PACKED && staged) {
+        __shared__ long long rows_lo[kBlock / 64], rows_hi[kBlock / 64];
+        long long lo = LLONG_MAX, hi = LLONG_MIN;
+        if (threadIdx.x < nb) {
+            lo = row_off[blk0 + threadIdx.x];
+            hi = lo + min<int>(plies[blk0 + threadIdx.x], OTH_MOVES_STRIDE) + 1;
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo = min(lo, __shfl_xor(lo, off));
+            hi = max(hi, __shfl_xor(hi, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            rows_lo[threadIdx.x >> 6] = lo;
+            rows_hi[threadIdx.x >> 6] = hi;
+        }
+        __syncthreads();
+        for (int w = 0; w < kBlock / 64; w++) {
+            lo = min(lo, rows_lo[w]);
+            hi = max(hi, rows_hi[w]);
+        }
+        base = lo;
+        bytes = hi - lo;
+    } else if (PACKED) {
+        base = row_off[blk0];
     }
+    const int64_t base_al = PACKED ? (base & ~(int64_t)15) : base;
     const int lead = (int)(base - base_al);  // stage bytes before the block's first (packed only)
     const int64_t span = lead + bytes;
-    const bool direct = PACKED && staged && (bytes < 0 || span > kReplayStagePacked);
+    const bool direct = PACKED && staged && span > kReplayStagePacked;
     if (staged && !direct) {  // rows past plies (strided) and any gap (packed) are staged as 0
         for (int c = lane; c < (PACKED ? kReplayStagePacked : kReplayStage) / 16; c += kBlock)
             replay_stage4[c] = make_uint4(0, 0, 0, 0);
@@ -1128,9 +1141,8 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                     if (q0 + q < lead || q0 + q >= span) continue;
                     const u32 byte = w[q >> 2] >> (8 * (q & 3)) & 0xffu;
                     if ((byte & kTurnEscape) != kTurnEscape) continue;
-                    uint8_t tb, eb;
-                    unstage_byte(byte, start_turn, game_of(q0 + q), tb, eb);
-                    tw[q >> 2] = (tw[q >> 2] & ~(0xffu << (8 * (q & 3)))) | ((u32)tb << (8 * (q & 3)));
+                    const u32 tb = start_turn[game_of(q0 + q)];
+                    tw[q >> 2] = (tw[q >> 2] & ~(0xffu << (8 * (q & 3)))) | (tb << (8 * (q & 3)));
                 }
             }
             const int64_t g0 = base_al + q0;  // global byte of the chunk's first
@@ -1147,10 +1159,11 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
         }
     } else {  // a caller's output that is not 16-B aligned: coalesced byte stores
         for (int64_t o = lead + lane; o < span; o += kBlock) {
-            uint8_t tb, eb;
-            unstage_byte(stage[o], start_turn, game_of(o), tb, eb);
+            const u32 c = stage[o];
+            // only an escaped turn needs its game (a search of the row offsets)
+            const uint8_t tb = (c & kTurnEscape) == kTurnEscape ? start_turn[game_of(o)] : (uint8_t)(c & kTurnEscape);
             if (pos_turn) pos_turn[base_al + o] = tb;
-            if (pos_end) pos_end[base_al + o] = eb;
+            if (pos_end) pos_end[base_al + o] = (uint8_t)(c >> 7);
         }
     }
 }

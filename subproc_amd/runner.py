@@ -60,10 +60,20 @@ def do_matches(conf, weights_a=None, n=1, seed=0, game_id0=0, weights_b=None, po
     r = ops.rollout_runner(n, seed, game_id0, policy, wa, wb, n_rand_a, n_rand_b, swap, record_moves=record,
                            device=device)
     a_black = r.a_black.cpu().numpy().astype(bool)
-    hp = hamlet_param_line(name_a, policy, wa) if name_a == "Hamlet" else (
-        hamlet_param_line(name_b, policy, wb) if name_b == "Hamlet" else "No Hamlet")
-    meta = [{"proc_a": name_a if ab else name_b, "proc_b": name_b if ab else name_a, "hamletparam": hp}
-            for ab in a_black]
+    # extract_hamlet_param (game_runner.py:124-130): Black's engine first, then
+    # White's, per game (the colours follow the swap draw)
+    line = {"a": hamlet_param_line(name_a, policy, wa), "b": hamlet_param_line(name_b, policy, wb)}
+
+    def hamlet(black, white):
+        for who, name in (black, white):
+            if name == "Hamlet":
+                return line[who]
+        return "No Hamlet"
+
+    meta = []
+    for ab in a_black:
+        black, white = (("a", name_a), ("b", name_b)) if ab else (("b", name_b), ("a", name_a))
+        meta.append({"proc_a": black[1], "proc_b": white[1], "hamletparam": hamlet(black, white)})
     diff = r.diff.cpu().numpy().astype(int)
     won = [("Black", m["proc_a"]) if d > 0 else (("White", m["proc_b"]) if d < 0 else ("None", ""))
            for d, m in zip(diff, meta)]

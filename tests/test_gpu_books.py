@@ -205,3 +205,38 @@ def test_replay_rows_odd_offsets_and_outputs():
         untouched[rows] = False
         assert bool((t[1:1 + total][untouched] == 0xAB).all()) and bool((e[1:1 + total][untouched] == 0xCD).all())
         assert int(t[0]) == 0xAB and bool((t[1 + total:] == 0xAB).all())
+
+
+def test_replay_rows_non_monotonic_offsets():
+    """Row offsets that are not increasing: games laid out in
+    reverse order, shuffled inside each 256-game block (the block's rows still
+    one range: staged), and shuffled over the whole launch (ranges overrun the
+    stage: direct).  The stage range is taken over every game of a block, so
+    every game's rows equal the strided table's, with aligned and +1 outputs."""
+    from subproc_amd import _lib
+    n = 1500
+    r = ops.rollout(n, 11, 77, record_moves=True, device="cuda")
+    full = ops.replay(r.moves, r.plies)
+    pl = r.plies.long()
+    inside = torch.arange(129, device="cuda")[None, :] <= pl[:, None]
+    cnt = (pl + 1).cpu().numpy()
+    rng = np.random.default_rng(9)
+    within = np.concatenate([rng.permutation(np.arange(b, min(b + 256, n))) for b in range(0, n, 256)])
+    L = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    total = int(cnt.sum())
+    for order in (np.arange(n)[::-1], within, rng.permutation(n)):
+        # game order[k] is the k-th in memory: disjoint rows, offsets out of order
+        off_np = np.zeros(n, np.int64)
+        off_np[order] = np.cumsum(cnt[order]) - cnt[order]
+        off = torch.as_tensor(off_np).cuda()
+        for shift in (0, 1):
+            b = torch.full((total, 2), 7, dtype=torch.int64, device="cuda")
+            t = torch.full((total + 1,), 0xAB, dtype=torch.uint8, device="cuda")
+            e = torch.full((total + 1,), 0xCD, dtype=torch.uint8, device="cuda")
+            assert L.oth_replay_rows(None, None, r.moves.data_ptr(), r.plies.data_ptr(), off.data_ptr(),
+                                     b.data_ptr(), t.data_ptr() + shift, e.data_ptr() + shift, n, s) == 0
+            rows = (off[:, None] + torch.arange(129, device="cuda")[None, :])[inside]
+            assert torch.equal(b[rows], full.boards[inside])
+            tt, ee = t[shift:shift + total], e[shift:shift + total]
+            assert torch.equal(tt[rows], full.turn[inside]) and torch.equal(ee[rows], full.end[inside])

@@ -99,3 +99,23 @@ def test_do_matches_books_meta_and_stats():
     assert mb.stats == ref_stats.store_batch_stats(books, reference_rule=True)
     w, l, dr = runner.wins_of_a(mb)
     assert w + l + dr == n
+
+
+def test_hamletparam_is_blacks_engine_first():
+    """GameRunner.extract_hamlet_param (game_runner.py:124-130) asks Black's
+    engine first: with both players named Hamlet the parameter line is the one
+    of whoever played Black in that game (the colours follow the swap draw)."""
+    conf = {"proc_randomize_black_white": 1}
+    wa = np.full((4, 9), 3, np.int8)
+    n = 64
+    mb = runner.do_matches(conf, wa, n, seed=23, name_a="Hamlet", name_b="Hamlet")
+    line_a = runner.hamlet_param_line("Hamlet", "eval", wa)
+    line_b = runner.hamlet_param_line("Hamlet", "eval", DEFAULT_WEIGHTS)
+    assert line_a != line_b
+    assert 0 < int(mb.a_black.sum()) < n
+    for g in range(n):
+        assert mb.meta[g]["hamletparam"] == (line_a if mb.a_black[g] else line_b)
+    mb = runner.do_matches(conf, wa, n, seed=23, name_a="GPU", name_b="Hamlet")
+    assert all(m["hamletparam"] == line_b for m in mb.meta)
+    mb = runner.do_matches(conf, wa, n, seed=23, name_a="X", name_b="Y")
+    assert all(m["hamletparam"] == "No Hamlet" for m in mb.meta)

@@ -21,9 +21,9 @@
  * Ownership / errors / threading:
  *   - every pointer is DEVICE memory owned by the caller (e.g. torch tensors);
  *     the library keeps no device state (the rollouts' work counter is a
- *     word the caller passes in, see oth_rollout) and allocates only a small
- *     stream-ordered scratch table inside oth_td_lookup / oth_td_merge
- *     (hipMallocAsync, freed on the same stream);
+ *     word the caller passes in, see oth_rollout) and allocates nothing:
+ *     the TD calls that need scratch (oth_td_sort_pairs, oth_td_lookup,
+ *     oth_td_merge) take it from the caller, with a size query;
  *   - calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
  *     and thread-safe on distinct streams; they may be captured in a hipGraph;
  *   - return value: OTH_OK (0), OTH_EINVAL (invalid argument, nothing launched),
@@ -258,9 +258,12 @@ int oth_eval(const uint64_t* boards, const uint8_t* side, const int8_t* weights,
  * negation (41-42).  base (n, exclusive prefix sum of 2*(plies+1)) and lam_pow
  * (OTH_POS_STRIDE doubles, lam_pow[k] = l ** k as the host computes it) are
  * device arrays. */
-#define OTH_TD_KEY_BITS 54
-/* packed counts() key: discs << 47 | moves << 40 | regions a..h, 5 bits each
- * from bit 35 down to bit 0.  Integer order == tuple order. */
+#define OTH_TD_KEY_BITS 43
+/* packed counts() key, each field as wide as its largest value: discs (0..64,
+ * 7 bits) << 36 | moves (0..63, 6 bits) << 30 | the regions a..h (sizes 4, 8,
+ * 4, 8, 8, 16, 4, 12: 3, 4, 3, 4, 4, 5, 3, 4 bits) at bits 27, 23, 20, 16,
+ * 12, 7, 4, 0.  Integer order == tuple order; 43 bits are 5 radix passes of
+ * the sort where the round-3 layout's 54 (5 bits per region) were 6. */
 int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
                    int64_t* keys, double* values, int64_t n, void* stream);
 /* oth_td_updates over an oth_replay_rows table: game g's position p is row
@@ -331,9 +334,14 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
 /* The batch's keys in the table: old_keys (n_old, unique, ascending) with
  * old_vals, upd_keys (n_upd, unique, ascending).  init[j] = the table value of
  * upd_keys[j], 0.0 if absent (a fresh key reads as 0, 53-56); is_new[j] = 1
- * if absent, else 0 (its cumsum is oth_td_merge's new_before). */
+ * if absent, else 0 (its cumsum is oth_td_merge's new_before).
+ * temp / temp_bytes: device scratch for the merge path's tile splits, as
+ * oth_td_sort_pairs: temp == NULL is a size query (*temp_bytes is set from
+ * n_old and n_upd alone; nothing is read or launched); otherwise *temp_bytes
+ * must be at least that size (any non-NULL temp when it is 0).  The library
+ * allocates nothing. */
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
-                  int64_t n_upd, double* init, uint8_t* is_new, void* stream);
+                  int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream);
 
 /* The batch's results into the table: old_keys (n_old, unique, ascending) with
  * old_vals, and upd_keys (n_upd, unique, ascending) with their new values
@@ -346,10 +354,11 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
  * (progress_position_moves_learn.py:58-62) for a whole batch.
  * new_before must be the exclusive cumsum of oth_td_lookup's is_new for the
  * same two key lists: for any other array the GPU build's output is undefined
- * (slots may stay unwritten), while the host build returns OTH_EINVAL. */
+ * (slots may stay unwritten), while the host build returns OTH_EINVAL.
+ * temp / temp_bytes: as oth_td_lookup's (its own size query). */
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
-                 double* out_vals, void* stream);
+                 double* out_vals, void* temp, size_t* temp_bytes, void* stream);
 
 #ifdef __cplusplus
 }

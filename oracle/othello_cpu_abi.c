@@ -210,7 +210,7 @@ int oth_features(const uint64_t* boards, const uint8_t* side, uint8_t* out, int6
 
 /* TD update stream over the oracle's counts() (see include/othello.h) */
 static int64_t td_key(const uint8_t f[10]) {
-    static const int shift[10] = {47, 40, 35, 30, 25, 20, 15, 10, 5, 0};
+    static const int shift[10] = {36, 30, 27, 23, 20, 16, 12, 7, 4, 0};  /* include/othello.h OTH_TD_KEY layout */
     int64_t k = 0;
     for (int i = 0; i < 10; i++) k |= (int64_t)f[i] << shift[i];
     return k;
@@ -344,8 +344,9 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
     memset(partials, 0, sizeof(double) * OTH_TD_FIT_BLOCKS * OTH_TD_FIT_COLS);
     for (int64_t i = 0; i < n; i++) {
         double x[9];
-        x[0] = (double)((keys[i] >> 40) & 127);
-        for (int r = 0; r < 8; r++) x[1 + r] = (double)((keys[i] >> (35 - 5 * r)) & 31);
+        /* counts()[1..9] of the key (include/othello.h OTH_TD_KEY layout) */
+        static const int shift[9] = {30, 27, 23, 20, 16, 12, 7, 4, 0}, width[9] = {6, 3, 4, 3, 4, 4, 5, 3, 4};
+        for (int f = 0; f < 9; f++) x[f] = (double)((keys[i] >> shift[f]) & ((1 << width[f]) - 1));
         if (!mean) {
             partials[0] += 1.0;
             for (int f = 0; f < 9; f++) partials[1 + f] += x[f];
@@ -364,10 +365,14 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
 
 /* each batch key in the table by a two-pointer walk */
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
-                  int64_t n_upd, double* init, uint8_t* is_new, void* stream) {
+                  int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream) {
     (void)stream;
-    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
-        (n_upd > 0 && (!upd_keys || !init || !is_new)))
+    if (n_old < 0 || n_upd < 0 || !temp_bytes) return OTH_EINVAL;
+    if (!temp) { /* size query: the two-pointer walk needs no scratch */
+        *temp_bytes = 0;
+        return OTH_OK;
+    }
+    if ((n_old > 0 && (!old_keys || !old_vals)) || (n_upd > 0 && (!upd_keys || !init || !is_new)))
         return OTH_EINVAL;
     int64_t i = 0;
     for (int64_t j = 0; j < n_upd; j++) {
@@ -383,9 +388,14 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
  * the GPU kernel's placement input and is only bounds-checked here) */
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
-                 double* out_vals, void* stream) {
+                 double* out_vals, void* temp, size_t* temp_bytes, void* stream) {
     (void)stream;
-    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+    if (n_old < 0 || n_upd < 0 || !temp_bytes) return OTH_EINVAL;
+    if (!temp) { /* size query: the two-pointer merge needs no scratch */
+        *temp_bytes = 0;
+        return OTH_OK;
+    }
+    if ((n_old > 0 && (!old_keys || !old_vals)) ||
         (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) || (n_old + n_upd > 0 && (!out_keys || !out_vals)))
         return OTH_EINVAL;
     const int64_t n_out = n_old + (n_upd > 0 ? new_before[n_upd] : 0);

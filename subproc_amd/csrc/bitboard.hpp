@@ -357,13 +357,56 @@ __device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
     R[5] = andn(0x0002040810204080ull << rsq, rev64(le));          // -7: normal files > x
 }
 
+// The same six rays as a constant table, built at compile time (rows as
+// ray_table_init's 0..5), read with one address per lane from the vector
+// cache instead of ~25 VALU of rays_of (OTH_STEP_RAYTAB).
+constexpr u64 rev64c(u64 x) {
+    u64 r = 0;
+    for (int i = 0; i < 64; i++)
+        if (x >> i & 1ull) r |= 1ull << (63 - i);
+    return r;
+}
+constexpr u64 ray_fromc(int sq, int dx, int dy) {
+    u64 r = 0;
+    int x = sq & 7, y = sq >> 3;
+    for (;;) {
+        x += dx;
+        y += dy;
+        if (x < 0 || x > 7 || y < 0 || y > 7) break;
+        r |= 1ull << (x + 8 * y);
+    }
+    return r;
+}
+struct RayConst {
+    u64 r[kRayRows * 64];
+};
+constexpr RayConst make_ray_const() {
+    RayConst t{};
+    const int dx[6] = {0, 1, -1, 0, -1, 1}, dy[6] = {1, 1, 1, -1, -1, -1};
+    for (int row = 0; row < kRayRows; row++)
+        for (int sq = 0; sq < 64; sq++) {
+            const u64 r = ray_fromc(sq, dx[row], dy[row]);
+            t.r[row * 64 + sq] = row < 3 ? r : rev64c(r);
+        }
+    return t;
+}
+__constant__ const RayConst kRayConst = make_ray_const();
+
 // flips of the move on empty square sq (Board.put's count is their popcount,
 // board.py:161-174); 0 when nothing is flanked.  Horizontal runs by the carry
 // on the inner files (no ray mask needed), the six others by ray_flips; rays
 // leaving in decreasing bit order on the bit-reversed board.
+#ifndef OTH_STEP_RAYTAB
+#define OTH_STEP_RAYTAB 0
+#endif
 __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     u64 R[kRayRows];
+#if OTH_STEP_RAYTAB
+#pragma unroll
+    for (int i = 0; i < kRayRows; i++) R[i] = kRayConst.r[i * 64 + sq];
+#else
     rays_of(sq, R);
+#endif
     const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
     const u64 rP = rev64(P), rO = rev64(O);
     const u64 Oi = and2(O, INNER_FILES), rOi = and2(rO, INNER_FILES);

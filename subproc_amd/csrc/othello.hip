@@ -108,10 +108,14 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // 1-ply policies (greedy: minimise the opponent's mobility on the child; eval:
 // maximise the mover's linear eval of the child; ties -> lowest square, the
 // first in puttables order).  A child's score is a key whose minimum is the
-// choice: (score << 6) | square.
+// choice: (score << 6) | square.  The child's boards (mover P2, opponent O2)
+// come back too: the chosen child is the next position, so the choice needs
+// no second flip computation.
 template <int POLICY>
-__device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab) {
-    u64 P2 = P, O2 = O;
+__device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab,
+                                         u64& P2, u64& O2) {
+    P2 = P;
+    O2 = O;
     place(P2, O2, flips_rays(sq, s, rays));
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
     // every child has popcount(P|O) + 1 discs: one weight row per parent
@@ -125,16 +129,24 @@ __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq,
     return ((u32)((1 << 20) - v) << 6) | sq;
 }
 
-// one lane alone over its own children (w_tab: the mover's eval table)
+// one lane alone over its own children (w_tab: the mover's eval table); the
+// chosen child's boards into P2 / O2
 template <int POLICY>
-__device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, const u64* rays, const int* w_tab) {
+__device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, const u64* rays, const int* w_tab,
+                                           u64& P2, u64& O2) {
     u32 best = 0xFFFFFFFFu;
     u64 legal = pos.legal;
     const RunSets s = run_sets(pos);
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         legal &= legal - 1;
-        best = min(best, child_key<POLICY>(P, O, s, sq, rays, w_tab));
+        u64 cP, cO;
+        const u32 k = child_key<POLICY>(P, O, s, sq, rays, w_tab, cP, cO);
+        if (k < best) {
+            best = k;
+            P2 = cP;
+            O2 = cO;
+        }
     }
     return best & 63u;
 }
@@ -142,27 +154,30 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // Wave-cooperative choice.  A lane's own child loop makes the wave pay for its
 // busiest lane every ply (measured on greedy games: 662 child evaluations per
 // 64-game batch where 303 would do, 46% lane efficiency).  Instead the wave's
-// T children are spread over R = ceil(T / 64) rounds of all 64 lanes
-// (finished games included):
-//   * every choosing lane publishes its position (P, O, run sets) to the
-//     wave's LDS area, and evaluates its own children in its first rounds,
-//     taking them straight from its legal mask, lowest square first;
-//   * a lane with more than R children lists the surplus (its highest
-//     squares) in the wave's overflow list;
-//   * a lane with fewer than R children has R - (its children) free rounds,
-//     and the free rounds of the wave, numbered by an LDS atomic, take the
-//     overflow list entry of the same number;
-// and each child's key is folded into its parent's slot with an LDS atomicMin
-// (so the order in which children are evaluated does not matter).  Only the
-// surplus is listed: listing every child cost a per-lane loop as long as the
-// busiest lane's mobility.  A wave whose surplus exceeds the list (`cap`, at
-// most kCoopCap) falls back to lane_choose for that ply.
-constexpr int kCoopCap = 64 * 8;  // overflow entries per wave per ply
+// T children, numbered parent by parent in lane order (an exclusive scan of
+// the lanes' move counts), are cut into 64 consecutive chunks of
+// R = ceil(T / 64): lane i evaluates children R*i .. R*i + R - 1 in R rounds
+// (finished games included).  A lane finds its chunk's first parent by a
+// binary search of the scan in LDS and skips that parent's first children by
+// the k-th-bit pick; from there it walks the parents' legal masks lowest
+// square first, moving to the next parent with moves when one runs out.
+// Every choosing lane publishes its position (P, O, run sets) and legal mask
+// to the wave's LDS area; each child's key is folded into its parent's slot
+// with an LDS atomicMin (the order of evaluation does not matter), and the
+// evaluator whose key is the slot's minimum after its round writes the
+// child's boards to the parent's slot: the parent takes its next position
+// from there.  (Round 3 listed each lane's surplus children in an overflow
+// list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
+// chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
+// for every choosing lane instead.
 struct CoopWave {
-    u64 rec[64][10];          // parent lane: P, O, its RunSets (8 words)
-    uint16_t list[kCoopCap];  // overflow: (parent lane << 8) | (parent plays White) << 6 | square
+    u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words)
+    u64 legal[64];    // parent lane's legal mask (0: not choosing)
+    u64 win[64][2];   // the best child's boards so far: mover P2, opponent O2
+    u64 mine[64][2];  // the child this lane evaluated this round (parked across the round's sync)
+    u32 pre[64];      // exclusive scan of the move counts
     u32 best[64];
-    u32 total, over, free;    // children, overflow entries, free rounds of the wave this ply
+    uint8_t tbl[64];  // the parent's eval table (0 / 1)
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -174,80 +189,89 @@ __device__ __forceinline__ void load_parent(const u64* r, u64& P, u64& O, RunSet
     O = r[1];
     s = *reinterpret_cast<const RunSets*>(r + 2);
 }
+// inclusive scan over the wave's 64 lanes (DPP row shifts, then the row
+// broadcasts of lanes 15 and 31)
+__device__ __forceinline__ u32 wave_incl_scan(u32 x) {
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
 // w_s: the two eval tables (kEvalTable ints each); tbl (0 / 1) is the mover's
-// (Black's / White's, or in a GameRunner match player A's / B's)
+// (Black's / White's, or in a GameRunner match player A's / B's).  Returns
+// the chosen square of a choosing lane (64 otherwise); its child's boards are
+// left in cw.win[lane] (read them before the next call).
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
-                           const int* w_s, u32 lane, u32 cap) {
-    const u32 white = tbl ? 64u : 0u;  // (the list entry's table bit)
-    u32 cnt = 0;
+                           const int* w_s, const uint8_t* kth_tab, u32 lane, u32 cap) {
+    if (cap == 0) {
+        u32 result = 64;
+        if (need) {
+            u64 P2, O2;
+            result = lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0), P2, O2);
+            cw.win[lane][0] = P2;
+            cw.win[lane][1] = O2;
+        }
+        return result;
+    }
+    const u64 legal = need ? pos.legal : 0ull;
+    const u32 cnt = (u32)__popcll(legal);
+    const u32 incl = wave_incl_scan(cnt);
+    const u32 T = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    const u32 R = (T + 63u) >> 6;
+    cw.pre[lane] = incl - cnt;
+    cw.legal[lane] = legal;
     if (need) {
         u64* r = cw.rec[lane];
         r[0] = P;
         r[1] = O;
         *reinterpret_cast<RunSets*>(r + 2) = run_sets(pos);  // reversed once per parent, not per child
         cw.best[lane] = 0xFFFFFFFFu;
-        cnt = (u32)__popcll(pos.legal);
-        atomicAdd(&cw.total, cnt);
+        if (POLICY == OTH_POLICY_EVAL) cw.tbl[lane] = (uint8_t)tbl;
     }
     wave_sync();
-    const u32 rounds = (__builtin_amdgcn_readfirstlane(cw.total) + 63u) >> 6;
-    u64 m = need ? pos.legal : 0ull;
-    const u32 own = min(cnt, rounds);
-    u32 free_base = 0;
-    if (cnt > rounds) {
-        // the surplus, highest squares first, goes to the overflow list
-        const u32 extra = cnt - rounds;
-        u32 off = atomicAdd(&cw.over, extra);
-        const bool fits = off + extra <= cap;
-        for (u32 i = 0; i < extra; i++) {
-            const u32 sq = 63u - (u32)__clzll((long long)m);
-            m ^= 1ull << sq;
-            if (fits) cw.list[off++] = (uint16_t)((lane << 8) | white | sq);
+    // this lane's chunk of the children: [t0, t0 + cnt_mine)
+    const u32 t0 = R * lane, cnt_mine = t0 < T ? min(R, T - t0) : 0u;
+    u32 p = 0;
+    u64 m = 0;
+    if (cnt_mine) {
+        // the chunk's first parent: the last lane whose first child is <= t0
+#pragma unroll
+        for (u32 step = 32; step >= 1; step >>= 1)
+            if (cw.pre[p + step] <= t0) p += step;
+        m = cw.legal[p];
+        const u32 k0 = t0 - cw.pre[p];  // the parent's children before the chunk
+        if (k0) m &= ~0ull << kth_bit_tab(m, k0, (u32)__popc((u32)m), kth_tab);
+    }
+    for (u32 r = 0; r < R; r++) {
+        const bool have = r < cnt_mine;
+        u32 key = 0xFFFFFFFFu;
+        if (have) {
+            while (m == 0) m = cw.legal[++p];  // the next parent with moves (one exists: t0 + r < T)
+            const u32 sq = (u32)__ffsll((unsigned long long)m) - 1u;
+            m &= m - 1;
+            u64 Pp, Op;
+            RunSets ps;
+            load_parent(cw.rec[p], Pp, Op, ps);
+            const int* wt = w_s;
+            if (POLICY == OTH_POLICY_EVAL && cw.tbl[p]) wt += kEvalTable;
+            u64 cP, cO;
+            key = child_key<POLICY>(Pp, Op, ps, sq, rays, wt, cP, cO);
+            atomicMin(&cw.best[p], key);
+            cw.mine[lane][0] = cP;  // parked in LDS, not held in registers across the sync
+            cw.mine[lane][1] = cO;
         }
-    } else if (cnt < rounds) {
-        free_base = atomicAdd(&cw.free, rounds - cnt);
-    }
-    wave_sync();
-    const u32 over = __builtin_amdgcn_readfirstlane(cw.over);
-    u32 result = 64;
-    if (over > cap) {
-        if (need) result = lane_choose<POLICY>(pos, P, O, rays, w_s + (white ? kEvalTable : 0));
-    } else {
-        for (u32 k = 0; k < rounds; k++) {
-            u32 par = lane, sq = 0, wt = white;
-            bool have = k < own;
-            if (have) {  // an own child: the lowest square left
-                sq = (u32)__ffsll((unsigned long long)m) - 1u;
-                m &= m - 1;
-            } else {  // a free round: the overflow entry of its number, if any
-                const u32 j = free_base + (k - own);
-                if (j < over) {
-                    const u32 e = cw.list[j];
-                    par = e >> 8;
-                    sq = e & 63u;
-                    wt = e & 64u;
-                    have = true;
-                }
-            }
-            if (have) {
-                u64 Pp, Op;
-                RunSets ps;
-                load_parent(cw.rec[par], Pp, Op, ps);
-                atomicMin(&cw.best[par], child_key<POLICY>(Pp, Op, ps, sq, rays, w_s + (wt ? kEvalTable : 0)));
-            }
+        wave_sync();  // every lane's atomic of this round before the reads (a wave's LDS ops are in order)
+        if (have && cw.best[p] == key) {  // keys are unique per parent: one writer per improved slot
+            cw.win[p][0] = cw.mine[lane][0];
+            cw.win[p][1] = cw.mine[lane][1];
         }
-        wave_sync();
-        if (need) result = cw.best[lane] & 63u;
-    }
-    wave_sync();  // every lane has read the counters / best before the reset
-    if (lane == 0) {
-        cw.total = 0;
-        cw.over = 0;
-        cw.free = 0;
     }
     wave_sync();
-    return result;
+    return need ? cw.best[lane] & 63u : 64u;
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -487,7 +511,7 @@ struct RolloutArgs {
     int64_t n;
     unsigned long long* work;  // the caller's work word (0 at start, left at 0)
     u64 last_ticket;           // 64 * (batches + waves - 1): the launch's last dequeue
-    u32 coop_cap;              // 1-ply policies: overflow list entries used (kCoopCap; tests lower it)
+    u32 coop_cap;              // 1-ply policies: 0 = per-lane choice (lane_choose; tests), else cooperative
     EvalWeights ew[2];         // OTH_POLICY_EVAL only: Black's table, White's table (runner: A's, B's)
     // GameRunner schedule (RUNNER kernels, oth_rollout_runner): random budgets
     // of players A and B (already capped at 10), the colour draw, A's colours
@@ -536,11 +560,6 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     __shared__ u64 rays[kTabRows * 64];
     __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
-    if (POLICY != OTH_POLICY_RANDOM && threadIdx.x < kBlock / 64) {
-        coop[threadIdx.x].total = 0;
-        coop[threadIdx.x].over = 0;
-        coop[threadIdx.x].free = 0;
-    }
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
@@ -742,16 +761,21 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                         }
                     }
                 }
+                CoopWave& cw = coop[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];  // wave-uniform: an SGPR base
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
                     const u32 tbl = side == OTH_BLACK ? tbl_black : tbl_black ^ 1u;
-                    const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, coop[threadIdx.x >> 6], rays, w_s,
-                                                      (u32)lane, a.coop_cap);
+                    const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, cw, rays, w_s, kth_tab, (u32)lane,
+                                                      a.coop_cap);
                     if (choose) sq = c;
                 }
                 if (moving) {
-                    const Flips f = flips_rays(sq, run_sets(pos), rays);
                     if (RECORD) rec_put(ply, (uint8_t)sq);
-                    place(P, O, f);
+                    if (choose) {  // the child the choice evaluated is the next position (the
+                        P = cw.win[lane][0];  // slot is rewritten only by the next ply's choice)
+                        O = cw.win[lane][1];
+                    } else {  // a random move (the first plies, or go_for's coin)
+                        place(P, O, flips_rays(sq, run_sets(pos), rays));
+                    }
                     const u64 np = O;
                     O = P;
                     P = np;
@@ -1358,9 +1382,11 @@ __global__ __launch_bounds__(kBlock) void eval_kernel(const u64* __restrict__ bo
 __device__ __forceinline__ int64_t td_key(ulonglong2 b, u32 sd) {
     u64 mine, mob;
     side_view(b, sd, mine, mob);
-    u64 k = ((u64)__popcll(b.x | b.y) << 47) | ((u64)__popcll(mob) << 40);
+    // include/othello.h OTH_TD_KEY_BITS layout
+    constexpr int kShift[8] = {27, 23, 20, 16, 12, 7, 4, 0};
+    u64 k = ((u64)__popcll(b.x | b.y) << 36) | ((u64)__popcll(mob) << 30);
 #pragma unroll
-    for (int r = 0; r < 8; r++) k |= (u64)__popcll(mine & kRegionMasks[r]) << (35 - 5 * r);
+    for (int r = 0; r < 8; r++) k |= (u64)__popcll(mine & kRegionMasks[r]) << kShift[r];
     return (int64_t)k;
 }
 
@@ -1512,52 +1538,125 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
 }
 
 // Speculative split of a very long segment (the opening position's key gets
-// one update per game and side) over the lanes of one wave.  The rule is a
-// contraction (|1 - a| < 1): two runs over the same values from different
-// states approach each other by |1 - a| per step and, once a rounding maps
-// them to the same double, stay equal.  So lane p > 0 guesses the state at
-// the start of its part by a warm-up run over the `warm` values before it,
-// from state 0 (the rule then starts at the first value itself); `warm` is
-// sized by the launcher so that |1 - a|^warm < 2^-64.  Lane p then runs its
-// part from the guess.  Lane 0 checks the guesses in order against the
-// verified end state of the part before, bit for bit: a part whose guess
-// matched has its lane's end state; one whose guess did not is rerun from the
-// verified state.  Every result is thus the sequential one; speculation only
-// decides how fast it comes.
-// (64 parts: 256 over a block of 4 waves measured slower, 0.80 against 0.73 ms
-// for the whole EMA of a 262,144-game batch)
-constexpr int kTdSpecLanes = 64;
-__global__ __launch_bounds__(kTdSpecLanes) void td_ema_spec_kernel(const double* __restrict__ vals,
-                                                         const int64_t* __restrict__ seg_off,
-                                                         const double* __restrict__ init, double a, double oma,
-                                                         double* __restrict__ out,
-                                                         const int64_t* __restrict__ long_idx, int64_t warm) {
-    __shared__ double guess[kTdSpecLanes], fin[kTdSpecLanes];
-    const int lane = threadIdx.x;
-    const int64_t s = long_idx[blockIdx.x];
-    const int64_t b = seg_off[s], e = seg_off[s + 1];
+// one update per game and side; the first plies' keys a fraction of that)
+// over up to kSpecParts lanes of one block.  The rule is a contraction
+// (|1 - a| < 1): two runs over the same values from different states approach
+// each other by |1 - a| per step and, once a rounding maps them to the same
+// double, stay equal.  So the lane of part p > 0 guesses the state at the
+// start of its part by a warm-up run over the `warm` values before it, from
+// state 0 (the rule then starts at the first value itself), or exactly, from
+// the key's initial state, when the part starts within `warm` of the segment;
+// `warm` is sized by the launcher so that |1 - a|^warm < 2^-64.  Lane p then
+// runs its part from the guess.  If every part's guess equals the end state
+// of the part before (checked by all lanes at once), every part ran from the
+// exact state and the last part's end is the sequential result; otherwise
+// lane 0 walks the parts in order and reruns those whose guess missed from
+// the verified state.  Every result is thus the sequential one; speculation
+// only decides how fast it comes.
+// A lane's chain is bound by the loads it keeps in flight (each lane streams
+// its own range): round 3 ran 64 parts per key of >= 2 * warm values each
+// with 48 loads in flight per lane, 5,500 steps for the opening key at ~70
+// ns each, and one launch per batch took 376-951 us (profiles/
+// r03_profile_summary.json).  Here parts are ~kSpecPart values (up to 256 of
+// them, 4 waves), so no lane runs more than kSpecPart + warm (~2,500) steps,
+// and each lane keeps kSpecRing chunks (80 values) in flight (6 would pass the
+// 256 architectural VGPRs into AGPRs).
+constexpr int kSpecParts = 256;   // lanes per block: parts of one key, at most
+constexpr int kSpecPart = 1024;   // values per part (fewer parts for shorter keys)
+constexpr int kSpecRing = 5;      // chunks of kTdChunk values in flight per lane
+// the rule over vals[i, e) from state v, one lane, kSpecRing chunks ahead
+__device__ __forceinline__ double td_range_deep(double v, const double* __restrict__ vals, int64_t i, const int64_t e,
+                                                double a, double oma) {
+    constexpr int W = kSpecRing * kTdChunk;
+    if (e - i < W) {
+        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
+        return v;
+    }
+    const int64_t last = e - 1;
+    double buf[kSpecRing][kTdChunk];
+#pragma unroll
+    for (int c = 0; c < kSpecRing; c++) td_load(buf[c], vals, i + c * kTdChunk, last);
+    for (; i + W <= e; i += W) {
+#pragma unroll
+        for (int c = 0; c < kSpecRing; c++) {
+            v = td_run_full(v, buf[c], a, oma);
+            td_load(buf[c], vals, i + W + c * kTdChunk, last);  // kSpecRing chunks ahead (clamped)
+        }
+    }
+    const int r = (int)(e - i);  // 0 .. W-1 values left, already in buf
+#pragma unroll
+    for (int c = 0; c < kSpecRing; c++) v = td_run(v, buf[c], r - c * kTdChunk, a, oma);
+    return v;
+}
+// the speculative split of long key s (segment [b, e), its state before the
+// batch v0) by the block's kSpecParts threads; returns with the block synced
+__device__ __forceinline__ void td_spec_key(const double* __restrict__ vals, int64_t s, int64_t b, int64_t e,
+                                            double v0, double a, double oma, double* __restrict__ out, int64_t warm,
+                                            double* guess, double* fin, int* missed) {
+    const int p = threadIdx.x;
     const int64_t n = e - b;
-    if (warm <= 0 || n < 4 * warm) return;  // td_ema_long_kernel's segment
-    // parts of len >= 2 * warm values (a warm-up stays inside the segment and
-    // costs at most half a part), up to one per lane, none empty
-    const int64_t cap = min<int64_t>(kTdSpecLanes, n / (2 * warm));
-    const int64_t len = (n + cap - 1) / cap;
-    const int parts = (int)((n + len - 1) / len);
-    if (lane < parts) {
-        const int64_t i = b + lane * len, j = min(i + len, e);
-        const double g = lane == 0 ? (init ? init[s] : 0.0) : td_range(0.0, vals, i - warm, i, a, oma);
-        guess[lane] = g;
-        fin[lane] = td_range(g, vals, i, j, a, oma);
+    const int64_t want = min<int64_t>(kSpecParts, (n + kSpecPart - 1) / kSpecPart);
+    const int64_t len = (n + want - 1) / want;
+    const int parts = (int)((n + len - 1) / len);  // none empty
+    if (p == 0) *missed = 0;
+    if (p < parts) {
+        const int64_t i = b + p * len, j = min(i + len, e);
+        // the warm-up: from the key's state at the segment start (exact), or
+        // from 0 over the `warm` values before the part
+        const int64_t ws = max(b, i - warm);
+        const double g = td_range_deep(ws == b ? v0 : 0.0, vals, ws, i, a, oma);
+        guess[p] = g;
+        fin[p] = td_range_deep(g, vals, i, j, a, oma);
     }
     __syncthreads();
-    if (lane == 0) {
-        double v = fin[0];
-        for (int p = 1; p < parts; p++) {
-            const int64_t i = b + p * len, j = min(i + len, e);
-            if (__double_as_longlong(guess[p]) == __double_as_longlong(v)) v = fin[p];
-            else v = td_range(v, vals, i, j, a, oma);  // the warm-up had not converged: rerun the part
+    if (p > 0 && p < parts && __double_as_longlong(guess[p]) != __double_as_longlong(fin[p - 1])) *missed = 1;
+    __syncthreads();
+    if (p == 0) {
+        double v = fin[parts - 1];
+        if (*missed) {  // rare: a warm-up had not converged; rerun from the first miss on
+            v = fin[0];
+            for (int q = 1; q < parts; q++) {
+                const int64_t i = b + q * len, j = min(i + len, e);
+                if (__double_as_longlong(guess[q]) == __double_as_longlong(v)) v = fin[q];
+                else v = td_range_deep(v, vals, i, j, a, oma);
+            }
         }
         out[s] = v;
+    }
+    __syncthreads();  // guess / fin / missed are free for the next key
+}
+// Persistent over the long keys: block k of G takes long keys k, k + G,
+// k + 2G, ... (the longest keys are the smallest, the opening's and the
+// first plies', so they land on different blocks), checks kSpecParts of them
+// at once and splits those of >= 4 * warm updates; the rest are
+// td_ema_long_kernel's.  (One block per long key, most of them exiting at
+// once, cost a block slot each at this kernel's one block per CU.)
+__global__ __launch_bounds__(kSpecParts) void td_ema_spec_kernel(const double* __restrict__ vals,
+                                                                 const int64_t* __restrict__ seg_off,
+                                                                 const double* __restrict__ init, double a, double oma,
+                                                                 double* __restrict__ out,
+                                                                 const int64_t* __restrict__ long_idx, int64_t n_long,
+                                                                 int64_t warm) {
+    __shared__ double guess[kSpecParts], fin[kSpecParts];
+    __shared__ int missed, n_list;
+    __shared__ int64_t list[kSpecParts];
+    if (warm <= 0) return;
+    const int64_t G = gridDim.x;
+    for (int64_t k0 = blockIdx.x; k0 < n_long; k0 += G * kSpecParts) {
+        if (threadIdx.x == 0) n_list = 0;
+        __syncthreads();
+        const int64_t k = k0 + (int64_t)threadIdx.x * G;
+        if (k < n_long) {
+            const int64_t s = long_idx[k];
+            if (seg_off[s + 1] - seg_off[s] >= 4 * warm) list[atomicAdd(&n_list, 1)] = s;
+        }
+        __syncthreads();
+        const int m = n_list;
+        for (int q = 0; q < m; q++) {
+            const int64_t s = list[q];
+            td_spec_key(vals, s, seg_off[s], seg_off[s + 1], init ? init[s] : 0.0, a, oma, out, warm, guess, fin,
+                        &missed);
+        }
     }
 }
 
@@ -1821,9 +1920,9 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
         policy == OTH_POLICY_RANDOM && n >= kBigLaunch ? t.random_big_blocks : t.resident_blocks[policy];
     const unsigned grid = (unsigned)std::min<int64_t>(max_blocks, (int64_t)resident);
     a.work = reinterpret_cast<unsigned long long*>(work);
-    // OTH_COOP_CAP (tests only) shrinks the cooperative overflow list, so the
-    // per-lane fallback of coop_choose runs from ordinary positions
-    a.coop_cap = (u32)std::min(std::max(env_int("OTH_COOP_CAP", kCoopCap), 0), kCoopCap);
+    // OTH_COOP_CAP=0 (tests only): every 1-ply choice by its own lane
+    // (lane_choose), so the per-lane path runs from ordinary positions
+    a.coop_cap = env_int("OTH_COOP_CAP", 1) == 0 ? 0u : 1u;
     a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
     hipStream_t st = (hipStream_t)stream;
     if (run) {
@@ -2025,8 +2124,8 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
                                                                          out, long_idx, warm);
     rc = launched();
     if (rc != OTH_OK || warm <= 0) return rc;
-    td_ema_spec_kernel<<<(unsigned)n_long, kTdSpecLanes, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
-                                                                         out, long_idx, warm);
+    td_ema_spec_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecParts, 0, (hipStream_t)stream>>>(
+        values, seg_off, init, a, one_minus_a, out, long_idx, n_long, warm);
     return launched();
 }
 

@@ -9,9 +9,10 @@
 //   oth_td_fit_moments: the sums of the learner's per-shard regression.
 //
 // The sort:
-// rocPRIM's onesweep radix sort of the pairs themselves over the key's 54 bits
-// (OTH_TD_KEY_BITS), in 6 passes of 9-bit digits (the gfx950 default takes 8
-// bits a pass, 7 passes: 2.11-2.13 against 1.93 ms for 32.2M pairs,
+// rocPRIM's onesweep radix sort of the pairs themselves over the key's 43 bits
+// (OTH_TD_KEY_BITS), in 5 passes of 9-bit digits.  Round 3's key spent 5 bits
+// on every region count and took 54 bits, 6 passes: 1.93 ms for 32.2M pairs
+// (the gfx950 default of 8 bits a pass took 7 passes, 2.11-2.13 ms,
 // tools/diag/sort_bits.hip; 10 bits ran 3.58 ms, 11 do not fit the LDS).
 // torch.sort of the keys with a permutation is 8 passes of (key, int64 index)
 // pairs plus a gather of the values by that permutation.
@@ -231,10 +232,11 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
 // its partial sums in its own row of `partials` (OTH_TD_FIT_COLS doubles); the
 // caller adds the OTH_TD_FIT_BLOCKS rows, in a fixed order: deterministic.
 constexpr int kFitBlock = 256;
+// counts()[1..9] of an OTH_TD_KEY (include/othello.h layout)
 __device__ __forceinline__ void td_features(int64_t k, double (&x)[9]) {
-    x[0] = (double)((k >> 40) & 127);
+    constexpr int kShift[9] = {30, 27, 23, 20, 16, 12, 7, 4, 0}, kWidth[9] = {6, 3, 4, 3, 4, 4, 5, 3, 4};
 #pragma unroll
-    for (int r = 0; r < 8; r++) x[1 + r] = (double)((k >> (35 - 5 * r)) & 31);
+    for (int f = 0; f < 9; f++) x[f] = (double)((k >> kShift[f]) & ((1 << kWidth[f]) - 1));
 }
 template <int NACC>
 __device__ __forceinline__ void block_sum_to_row(double (&acc)[NACC], double* row, double* lds) {
@@ -299,18 +301,19 @@ __global__ __launch_bounds__(kFitBlock) void td_fit_pass2_kernel(const int64_t* 
     block_sum_to_row(acc, partials + (int64_t)blockIdx.x * OTH_TD_FIT_COLS, lds);
 }
 
-// the tiles' merge-path splits (tiles + 1 of them) into a stream-ordered
-// scratch allocation the caller frees on the same stream after its kernel
+// the tiles' merge-path splits (tiles + 1 of them) into the caller's scratch
 hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t nB, int64_t tile, int64_t tiles,
-                        int64_t** split, hipStream_t stream) {
+                        int64_t* split, hipStream_t stream) {
     const int64_t ns = tiles + 1;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(split), (size_t)ns * sizeof(int64_t), stream);
-    if (e != hipSuccess) return e;
     td_splits_kernel<<<(unsigned)((ns + kMergeBlock - 1) / kMergeBlock), kMergeBlock, 0, stream>>>(A, nA, B, nB, tile,
-                                                                                                  ns, *split);
-    e = hipGetLastError();
-    if (e != hipSuccess) (void)hipFreeAsync(*split, stream);
-    return e;
+                                                                                                  ns, split);
+    return hipGetLastError();
+}
+// the split table's bytes for n merged positions in tiles of `tile` (0 when
+// nothing is merged)
+size_t split_bytes(int64_t n_old, int64_t n_upd, int64_t tile) {
+    if (n_upd <= 0) return 0;
+    return (size_t)((n_old + n_upd + tile - 1) / tile + 1) * sizeof(int64_t);
 }
 
 }  // namespace
@@ -330,28 +333,39 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
 }
 
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
-                  int64_t n_upd, double* init, uint8_t* is_new, void* stream) {
-    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
-        (n_upd > 0 && (!upd_keys || !init || !is_new)))
+                  int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream) {
+    if (n_old < 0 || n_upd < 0 || !temp_bytes) return OTH_EINVAL;
+    const size_t need = split_bytes(n_old, n_upd, kLookupTile);
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if ((n_old > 0 && (!old_keys || !old_vals)) || (n_upd > 0 && (!upd_keys || !init || !is_new)) ||
+        *temp_bytes < need)
         return OTH_EINVAL;
     if (n_upd == 0) return OTH_OK;
     const int64_t n = n_old + n_upd;
     const int64_t tiles = (n + kLookupTile - 1) / kLookupTile;
-    int64_t* split = nullptr;
-    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kLookupTile, tiles, &split, (hipStream_t)stream);
+    int64_t* split = static_cast<int64_t*>(temp);
+    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kLookupTile, tiles, split, (hipStream_t)stream);
     if (e != hipSuccess) return -(int)e;
     td_lookup_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(old_keys, old_vals, n_old, upd_keys,
                                                                               n_upd, split, init, is_new);
     e = hipGetLastError();
-    const hipError_t ef = hipFreeAsync(split, (hipStream_t)stream);
-    return e != hipSuccess ? -(int)e : (ef == hipSuccess ? OTH_OK : -(int)ef);
+    return e != hipSuccess ? -(int)e : OTH_OK;
 }
 
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
-                 double* out_vals, void* stream) {
-    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
-        (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) || (n_old + n_upd > 0 && (!out_keys || !out_vals)))
+                 double* out_vals, void* temp, size_t* temp_bytes, void* stream) {
+    if (n_old < 0 || n_upd < 0 || !temp_bytes) return OTH_EINVAL;
+    const size_t need = split_bytes(n_old, n_upd, kMergeTile);
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if ((n_old > 0 && (!old_keys || !old_vals)) || (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) ||
+        (n_old + n_upd > 0 && (!out_keys || !out_vals)) || *temp_bytes < need)
         return OTH_EINVAL;
     const int64_t n = n_old + n_upd;
     if (n == 0) return OTH_OK;
@@ -364,14 +378,13 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
         return e == hipSuccess ? OTH_OK : -(int)e;
     }
     const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
-    int64_t* split = nullptr;
-    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kMergeTile, tiles, &split, (hipStream_t)stream);
+    int64_t* split = static_cast<int64_t*>(temp);
+    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kMergeTile, tiles, split, (hipStream_t)stream);
     if (e != hipSuccess) return -(int)e;
     td_merge_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(
         old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, split, out_keys, out_vals);
     e = hipGetLastError();
-    const hipError_t ef = hipFreeAsync(split, (hipStream_t)stream);
-    return e != hipSuccess ? -(int)e : (ef == hipSuccess ? OTH_OK : -(int)ef);
+    return e != hipSuccess ? -(int)e : OTH_OK;
 }
 
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,

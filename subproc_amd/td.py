@@ -45,8 +45,11 @@ from .params import SHARDS
 A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
 LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
 LONG_MIN = 48  # updates per key from which oth_td_ema_split runs the key on a whole wave
-_SHIFTS = (47, 40, 35, 30, 25, 20, 15, 10, 5, 0)
-_WIDTH = (7, 7, 5, 5, 5, 5, 5, 5, 5, 5)
+# include/othello.h OTH_TD_KEY layout: each field as wide as its largest value
+# (discs 0..64, moves 0..63, region counts up to the region sizes 4, 8, 4, 8,
+# 8, 16, 4, 12)
+_SHIFTS = (36, 30, 27, 23, 20, 16, 12, 7, 4, 0)
+_WIDTH = (7, 6, 3, 4, 3, 4, 4, 5, 3, 4)
 
 
 def lam_pow_table(lam=LAMBDA):
@@ -98,6 +101,15 @@ def records_plan(books, lam=LAMBDA):
     slot = {k: i for i, k in enumerate(uniq)}
     return (strings, np.array(term, np.int64), np.array([slot[k] for k in expo], np.int32),
             np.array([lam ** k for k in uniq], np.float64))
+
+
+def _with_scratch(fn, args, stream, device, what):
+    """Call a TD entry point that takes caller scratch (temp, temp_bytes): its
+    size query, the scratch from torch's caching allocator, the call."""
+    tb = ctypes.c_size_t(0)
+    check(fn(*args, None, ctypes.byref(tb), stream), what + " (size query)")
+    temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=device)
+    check(fn(*args, temp.data_ptr(), ctypes.byref(tb), stream), what)
 
 
 class StateMap:
@@ -208,8 +220,9 @@ class StateMap:
             if len(self):
                 init = torch.empty(n_upd, dtype=torch.float64, device=self.device)
                 is_new = torch.empty(n_upd, dtype=torch.uint8, device=self.device)
-                check(lib.oth_td_lookup(self.keys.data_ptr(), self.values.data_ptr(), len(self), ukeys.data_ptr(),
-                                        n_upd, init.data_ptr(), is_new.data_ptr(), stream), "oth_td_lookup")
+                _with_scratch(lib.oth_td_lookup, (self.keys.data_ptr(), self.values.data_ptr(), len(self),
+                                                  ukeys.data_ptr(), n_upd, init.data_ptr(), is_new.data_ptr()),
+                              stream, self.device, "oth_td_lookup")
             else:
                 init = torch.zeros(n_upd, dtype=torch.float64, device=self.device)
             out = torch.empty_like(init)
@@ -235,9 +248,9 @@ class StateMap:
         n_new = int(new_before[-1])
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
-        check(lib.oth_td_merge(self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(), out.data_ptr(),
-                               new_before.data_ptr(), n_upd, keys.data_ptr(), vals.data_ptr(), stream),
-              "oth_td_merge")
+        _with_scratch(lib.oth_td_merge, (self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(),
+                                         out.data_ptr(), new_before.data_ptr(), n_upd, keys.data_ptr(), vals.data_ptr()),
+                      stream, self.device, "oth_td_merge")
         self.keys, self.values = keys, vals
 
     def update_from_books(self, books):

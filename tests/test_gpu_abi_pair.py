@@ -44,6 +44,27 @@ def both(name, *args):
     torch.cuda.synchronize()
 
 
+def both_scratch(name, *args):
+    """`both` for the entry points that take caller scratch (temp, temp_bytes):
+    each library's own size query, then the call with that much scratch."""
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    stream = torch.cuda.current_stream().cuda_stream
+    ha = [HOSTP(a.h) if isinstance(a, Buf) else a for a in args]
+    da = [a.d.data_ptr() if isinstance(a, Buf) else a for a in args]
+    for lib, a, st in ((cpu, ha, None), (gpu, da, stream)):
+        tb = ctypes.c_size_t(0)
+        assert getattr(lib, name)(*a, None, ctypes.byref(tb), st) == 0, name
+        if lib is gpu:
+            temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=DEV)
+            tp = temp.data_ptr()
+        else:
+            temp = np.zeros(max(tb.value, 1), np.uint8)
+            tp = HOSTP(temp)
+        assert getattr(lib, name)(*a, tp, ctypes.byref(tb), st) == 0, name
+        if lib is gpu:
+            torch.cuda.synchronize()
+
+
 def work():
     """A rollout work word for both builds (include/othello.h: 0 at the call)."""
     return Buf(np.zeros(1, np.uint64))
@@ -76,12 +97,12 @@ def sort_pair(keys, vals, keys_out, vals_out, n):
 
 @pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
 def test_td_sort_pairs_stable(n, distinct):
-    """Keys over all 54 key bits with many repeats: both builds sort stably (values
-    are the stream positions, so any reordering of equal keys shows)."""
+    """Keys over all OTH_TD_KEY_BITS key bits with many repeats: both builds sort
+    stably (values are the stream positions, so any reordering of equal keys shows)."""
     rng = np.random.default_rng(n)
-    pool = rng.integers(0, 1 << 54, size=distinct, dtype=np.int64)
+    pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
     pool[0] = 0
-    pool[-1] = (1 << 54) - 1
+    pool[-1] = (1 << _lib.TD_KEY_BITS) - 1
     k = pool[rng.integers(0, distinct, size=n)]
     keys, vals = Buf(k), Buf(np.arange(n, dtype=np.float64))
     ko, vo = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64))
@@ -113,13 +134,13 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
     # the lookup that precedes the EMA: the batch keys' table values and new flags
     init, is_new = Buf(np.full(len(upd), 9.0)), Buf(np.full(len(upd), 7, np.uint8))
-    both("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
+    both_scratch("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
     same(init, is_new)
     np.testing.assert_array_equal(is_new.h, new.astype(np.uint8))
     olddict = dict(zip(old.tolist(), ov.tolist()))
     assert init.h.tolist() == [olddict.get(k, 0.0) for k in upd.tolist()]
     out_k, out_v = Buf(np.full(n_out, -7, np.int64)), Buf(np.zeros(n_out))
-    both("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
+    both_scratch("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
     same(out_k, out_v)
     assert out_k.h.tolist() == sorted(want)
     assert out_v.h.tolist() == [want[k] for k in sorted(want)]
@@ -150,12 +171,12 @@ def test_td_merge_pair_skewed(shape):
     nb = np.concatenate([[0], np.cumsum(new)]).astype(np.int64)
     ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
     init, is_new = Buf(np.full(len(upd), 9.0)), Buf(np.full(len(upd), 7, np.uint8))
-    both("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
+    both_scratch("oth_td_lookup", ok, ovb, len(old), uk, len(upd), init, is_new)
     same(init, is_new)
     np.testing.assert_array_equal(is_new.h, new.astype(np.uint8))
     n_out = len(old) + int(nb[-1])
     out_k, out_v = Buf(np.full(n_out, -7, np.int64)), Buf(np.zeros(n_out))
-    both("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
+    both_scratch("oth_td_merge", ok, ovb, len(old), uk, uvb, nbb, len(upd), out_k, out_v)
     same(out_k, out_v)
     want = dict(zip(old.tolist(), ov.tolist()))
     want.update(zip(upd.tolist(), uv.tolist()))
@@ -382,20 +403,26 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_sort_pairs(None, None, None, None, -1, None, ctypes.byref(tb), s) == E
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, None, None, s) == E  # no size
         assert lib.oth_td_sort_pairs(None, None, None, None, 5, ctypes.c_void_p(8), ctypes.byref(tb), s) == E
-        assert lib.oth_td_merge(None, None, 0, None, None, None, 0, None, None, s) == 0
-        assert lib.oth_td_lookup(None, None, 5, None, 0, None, None, s) == E  # table without pointers
-        assert lib.oth_td_lookup(None, None, 0, None, 0, None, None, s) == 0
-        assert lib.oth_td_lookup(None, None, 0, None, 3, None, None, s) == E
+        tb, one = ctypes.c_size_t(0), ctypes.c_void_p(8)
+        assert lib.oth_td_merge(None, None, 0, None, None, None, 0, None, None, one, ctypes.byref(tb), s) == 0
+        assert lib.oth_td_merge(None, None, 0, None, None, None, 0, None, None, one, None, s) == E  # no size
+        assert lib.oth_td_lookup(None, None, 5, None, 0, None, None, one, ctypes.byref(tb), s) == E  # table w/o pointers
+        assert lib.oth_td_lookup(None, None, 0, None, 0, None, None, one, ctypes.byref(tb), s) == 0
+        assert lib.oth_td_lookup(None, None, 0, None, 3, None, None, one, ctypes.byref(tb), s) == E
+        # size queries read nothing but the counts
+        assert lib.oth_td_lookup(None, None, 10_000, None, 7_000, None, None, None, ctypes.byref(tb), s) == 0
+        assert tb.value >= 8 or lib is not _lib.load()
+        assert lib.oth_td_merge(None, None, 10_000, None, None, None, 7_000, None, None, None, ctypes.byref(tb), s) == 0
         assert lib.oth_td_fit_moments(None, None, 3, None, ctypes.c_void_p(8), s) == E
         assert lib.oth_td_fit_moments(None, None, 0, None, None, s) == E  # no partials
-        assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, s) == E
-        assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, s) == E
-        assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, s) == E
+        assert lib.oth_td_merge(None, None, -1, None, None, None, 0, None, None, one, ctypes.byref(tb), s) == E
+        assert lib.oth_td_merge(None, None, 3, None, None, None, 0, None, None, one, ctypes.byref(tb), s) == E
+        assert lib.oth_td_merge(None, None, 0, None, None, None, 3, None, None, one, ctypes.byref(tb), s) == E
     # a batch with no keys: the table is copied, new_before is not needed (NULL)
     old = Buf(np.array([3, 8, 40], np.int64))
     ov = Buf(np.array([0.5, -2.0, 7.25]))
     ok, ovo = Buf(np.zeros(3, np.int64)), Buf(np.zeros(3))
-    both("oth_td_merge", old, ov, 3, None, None, None, 0, ok, ovo)
+    both_scratch("oth_td_merge", old, ov, 3, None, None, None, 0, ok, ovo)
     same(ok, ovo)
     assert ok.h.tolist() == [3, 8, 40] and ovo.h.tolist() == [0.5, -2.0, 7.25]
     # every rollout output may be NULL: only the histogram is produced

@@ -4,6 +4,7 @@ header's oth_td_* against the fixture made with the reference's hash_from_book."
 import ctypes
 
 import numpy as np
+import pytest
 
 import oracle
 from golden_io import load_npz
@@ -24,13 +25,19 @@ def fixture_games():
 
 
 def test_key_packing():
-    for c in [(4, 4, 0, 0, 0, 0, 0, 0, 0, 2), (64, 0, 4, 8, 4, 8, 8, 16, 4, 12), (64, 99, 0, 0, 0, 0, 0, 0, 0, 0)]:
+    # every field at its largest value: discs 64, moves 63, the region sizes
+    for c in [(4, 4, 0, 0, 0, 0, 0, 0, 0, 2), (64, 0, 4, 8, 4, 8, 8, 16, 4, 12), (64, 63, 0, 0, 0, 0, 0, 0, 0, 0),
+              (64, 63, 4, 8, 4, 8, 8, 16, 4, 12)]:
         k = td.counts_to_key(c)
         assert td.key_to_counts(k) == c and k < (1 << _lib.TD_KEY_BITS)
         assert td.hash_string(k) == ":".join(map(str, c))
     # integer order == tuple order
-    cs = [(5, 3, 1, 0, 0, 0, 0, 0, 0, 0), (5, 3, 0, 9, 9, 9, 9, 9, 9, 9), (4, 40, 4, 8, 4, 8, 8, 16, 4, 12)]
+    cs = [(5, 3, 1, 0, 0, 0, 0, 0, 0, 0), (5, 3, 0, 8, 4, 8, 8, 16, 4, 12), (4, 40, 4, 8, 4, 8, 8, 16, 4, 12),
+          (5, 2, 4, 8, 4, 8, 8, 16, 4, 12), (5, 3, 0, 8, 4, 8, 8, 16, 4, 11)]
     assert sorted(cs) == sorted(cs, key=td.counts_to_key)
+    for bad in [(128, 0, 0, 0, 0, 0, 0, 0, 0, 0), (4, 64, 0, 0, 0, 0, 0, 0, 0, 0), (4, 4, 8, 0, 0, 0, 0, 0, 0, 0)]:
+        with pytest.raises(ValueError):
+            td.counts_to_key(bad)
 
 
 def test_lam_pow_is_cpython_pow():
@@ -95,7 +102,7 @@ def test_fit_matches_sklearn_on_fixture_states():
     part = np.zeros((_lib.TD_FIT_BLOCKS, _lib.TD_FIT_COLS))
     coef, icpt, n = np.zeros((4, 9)), np.zeros(4), np.zeros(4, np.int64)
     for k, (lo, hi) in enumerate(td.SHARDS):
-        s, e = np.searchsorted(keys, [lo << 47, (hi + 1) << 47])
+        s, e = np.searchsorted(keys, [lo << td._SHIFTS[0], (hi + 1) << td._SHIFTS[0]])
         n[k] = e - s
         if e == s:
             continue
@@ -135,13 +142,18 @@ def test_cpu_abi_td_merge():
     nb = np.concatenate([[0], np.cumsum(~np.isin(upd, old))]).astype(np.int64)
     n_out = len(old) + int(nb[-1])
     ok, vals = np.empty(n_out, np.int64), np.empty(n_out)
-    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals), None) == 0
+    tb = ctypes.c_size_t(7)
+    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals), None,
+                            ctypes.byref(tb), None) == 0 and tb.value == 0  # the host build needs no scratch
+    tmp = np.zeros(1, np.uint8)
+    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals), P(tmp),
+                            ctypes.byref(tb), None) == 0
     want = dict(zip(old.tolist(), ov.tolist()))
     want.update(zip(upd.tolist(), uv.tolist()))
     assert ok.tolist() == sorted(want) and vals.tolist() == [want[k] for k in sorted(want)]
     nb[-1] -= 1  # one new key too few: the output would overflow
-    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals),
-                            None) == _lib.OTH_EINVAL
+    assert lib.oth_td_merge(P(old), P(ov), len(old), P(upd), P(uv), P(nb), len(upd), P(ok), P(vals), P(tmp),
+                            ctypes.byref(tb), None) == _lib.OTH_EINVAL
 
 
 def test_cpu_abi_td_lookup():
@@ -150,5 +162,6 @@ def test_cpu_abi_td_lookup():
     ov = np.array([0.5, -1.0, 2.0, 3.5])
     upd = np.array([1, 5, 10, 11, 12], np.int64)
     init, is_new = np.full(5, 9.0), np.full(5, 7, np.uint8)
-    assert lib.oth_td_lookup(P(old), P(ov), 4, P(upd), 5, P(init), P(is_new), None) == 0
+    tb, tmp = ctypes.c_size_t(0), np.zeros(1, np.uint8)
+    assert lib.oth_td_lookup(P(old), P(ov), 4, P(upd), 5, P(init), P(is_new), P(tmp), ctypes.byref(tb), None) == 0
     assert init.tolist() == [0.0, -1.0, 0.0, 3.5, 0.0] and is_new.tolist() == [1, 0, 1, 0, 1]

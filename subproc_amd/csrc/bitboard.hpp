@@ -343,7 +343,9 @@ __device__ __forceinline__ u64 ray_flips(u64 first, u64 R, u64 P, u64 O) {
 // the square is 63 - sq and a file mask is the mirror (rev64) of its normal
 // counterpart.  ~20 VALU; the single-step kernel uses this instead of an LDS
 // table, whose per-block copy and barrier cost more than that
-// (tools/diag/launch_floor.py, step_ab.py).
+// (tools/diag/launch_floor.py, step_ab.py), or a constant table in global
+// memory: six more vector loads per board cost the HBM-bound step 159 ->
+// 182 us per 16M boards (round 4, tools/diag/step_ab.py).
 __device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
     constexpr u64 ONES = 0x0101010101010101ull;
     const u32 x = sq & 7u, rsq = sq ^ 63u;
@@ -357,56 +359,13 @@ __device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
     R[5] = andn(0x0002040810204080ull << rsq, rev64(le));          // -7: normal files > x
 }
 
-// The same six rays as a constant table, built at compile time (rows as
-// ray_table_init's 0..5), read with one address per lane from the vector
-// cache instead of ~25 VALU of rays_of (OTH_STEP_RAYTAB).
-constexpr u64 rev64c(u64 x) {
-    u64 r = 0;
-    for (int i = 0; i < 64; i++)
-        if (x >> i & 1ull) r |= 1ull << (63 - i);
-    return r;
-}
-constexpr u64 ray_fromc(int sq, int dx, int dy) {
-    u64 r = 0;
-    int x = sq & 7, y = sq >> 3;
-    for (;;) {
-        x += dx;
-        y += dy;
-        if (x < 0 || x > 7 || y < 0 || y > 7) break;
-        r |= 1ull << (x + 8 * y);
-    }
-    return r;
-}
-struct RayConst {
-    u64 r[kRayRows * 64];
-};
-constexpr RayConst make_ray_const() {
-    RayConst t{};
-    const int dx[6] = {0, 1, -1, 0, -1, 1}, dy[6] = {1, 1, 1, -1, -1, -1};
-    for (int row = 0; row < kRayRows; row++)
-        for (int sq = 0; sq < 64; sq++) {
-            const u64 r = ray_fromc(sq, dx[row], dy[row]);
-            t.r[row * 64 + sq] = row < 3 ? r : rev64c(r);
-        }
-    return t;
-}
-__constant__ const RayConst kRayConst = make_ray_const();
-
 // flips of the move on empty square sq (Board.put's count is their popcount,
 // board.py:161-174); 0 when nothing is flanked.  Horizontal runs by the carry
 // on the inner files (no ray mask needed), the six others by ray_flips; rays
 // leaving in decreasing bit order on the bit-reversed board.
-#ifndef OTH_STEP_RAYTAB
-#define OTH_STEP_RAYTAB 0
-#endif
 __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     u64 R[kRayRows];
-#if OTH_STEP_RAYTAB
-#pragma unroll
-    for (int i = 0; i < kRayRows; i++) R[i] = kRayConst.r[i * 64 + sq];
-#else
     rays_of(sq, R);
-#endif
     const u64 mv = 1ull << sq, rmv = 1ull << (63u - sq);
     const u64 rP = rev64(P), rO = rev64(O);
     const u64 Oi = and2(O, INNER_FILES), rOi = and2(rO, INNER_FILES);

@@ -170,11 +170,16 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
+#ifndef OTH_COOP_KEEP
+#define OTH_COOP_KEEP 1
+#endif
 struct CoopWave {
     u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words)
     u64 legal[64];    // parent lane's legal mask (0: not choosing)
+#if OTH_COOP_KEEP
     u64 win[64][2];   // the best child's boards so far: mover P2, opponent O2
     u64 mine[64][2];  // the child this lane evaluated this round (parked across the round's sync)
+#endif
     u32 pre[64];      // exclusive scan of the move counts
     u32 best[64];
     uint8_t tbl[64];  // the parent's eval table (0 / 1)
@@ -212,8 +217,10 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
         if (need) {
             u64 P2, O2;
             result = lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0), P2, O2);
+#if OTH_COOP_KEEP
             cw.win[lane][0] = P2;
             cw.win[lane][1] = O2;
+#endif
         }
         return result;
     }
@@ -261,14 +268,18 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
             u64 cP, cO;
             key = child_key<POLICY>(Pp, Op, ps, sq, rays, wt, cP, cO);
             atomicMin(&cw.best[p], key);
+#if OTH_COOP_KEEP
             cw.mine[lane][0] = cP;  // parked in LDS, not held in registers across the sync
             cw.mine[lane][1] = cO;
+#endif
         }
+#if OTH_COOP_KEEP
         wave_sync();  // every lane's atomic of this round before the reads (a wave's LDS ops are in order)
         if (have && cw.best[p] == key) {  // keys are unique per parent: one writer per improved slot
             cw.win[p][0] = cw.mine[lane][0];
             cw.win[p][1] = cw.mine[lane][1];
         }
+#endif
     }
     wave_sync();
     return need ? cw.best[lane] & 63u : 64u;
@@ -412,19 +423,37 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
     if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1);
 }
 
+#ifndef OTH_STEP_PER_THREAD
+#define OTH_STEP_PER_THREAD 1
+#endif
+constexpr int kStepPerThread = OTH_STEP_PER_THREAD;
+// kStepPerThread boards per thread, kBlock * gridDim apart (each load
+// instruction still coalesced), all loaded before any is computed
 __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, const uint8_t* turn_in,
                                                       const uint8_t* __restrict__ move, u64* boards_out,
                                                       uint8_t* turn_out, u64* __restrict__ flips_out,
                                                       u64* __restrict__ legal_next, int8_t* __restrict__ ret_out,
                                                       uint8_t* __restrict__ nturn, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(boards_in)[i];
-    const u32 t = turn_in[i], mvc = move[i];
-    // all three loads in flight together: without this hipcc sinks the move
-    // load into the valid-turn branch, a second dependent HBM round trip per wave
-    asm volatile("" ::"v"(t), "v"(mvc));
-    step_board(i, b, t, mvc, boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x, stride = (int64_t)gridDim.x * kBlock;
+    ulonglong2 b[kStepPerThread];
+    u32 t[kStepPerThread], mvc[kStepPerThread];
+#pragma unroll
+    for (int j = 0; j < kStepPerThread; j++) {
+        const int64_t i = i0 + j * stride;
+        if (i < n) {
+            b[j] = reinterpret_cast<const ulonglong2*>(boards_in)[i];
+            t[j] = turn_in[i];
+            mvc[j] = move[i];
+            // all the loads in flight together: without this hipcc sinks the move
+            // load into the valid-turn branch, a second dependent HBM round trip per wave
+            asm volatile("" ::"v"(t[j]), "v"(mvc[j]));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kStepPerThread; j++) {
+        const int64_t i = i0 + j * stride;
+        if (i < n) step_board(i, b[j], t[j], mvc[j], boards_out, turn_out, flips_out, legal_next, ret_out, nturn);
+    }
 }
 
 // hands_for_direc (board.py:124-139) for any origin and any direction: the
@@ -770,10 +799,13 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 if (moving) {
                     if (RECORD) rec_put(ply, (uint8_t)sq);
+#if OTH_COOP_KEEP
                     if (choose) {  // the child the choice evaluated is the next position (the
                         P = cw.win[lane][0];  // slot is rewritten only by the next ply's choice)
                         O = cw.win[lane][1];
-                    } else {  // a random move (the first plies, or go_for's coin)
+                    } else  // a random move (the first plies, or go_for's coin)
+#endif
+                    {
                         place(P, O, flips_rays(sq, run_sets(pos), rays));
                     }
                     const u64 np = O;
@@ -1862,8 +1894,8 @@ int oth_step(const uint64_t* boards_in, const uint8_t* turn_in, const uint8_t* m
              void* stream) {
     if (n < 0 || (n > 0 && (!boards_in || !turn_in || !move))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    step_kernel<<<blocks_for(n), kBlock, 0, (hipStream_t)stream>>>(boards_in, turn_in, move, boards_out, turn_out,
-                                                                   flips, legal_next, ret, nturn, n);
+    step_kernel<<<blocks_for((n + kStepPerThread - 1) / kStepPerThread), kBlock, 0, (hipStream_t)stream>>>(
+        boards_in, turn_in, move, boards_out, turn_out, flips, legal_next, ret, nturn, n);
     return launched();
 }
 

@@ -618,15 +618,14 @@ def _high_mobility_boards(m, seed, iters=400):
     return nb, cur
 
 
-@pytest.mark.parametrize("cap", [None, "64", "0"])
+@pytest.mark.parametrize("cap", [None, "0"])
 def test_greedy_eval_coop_overflow_fallback_vs_oracle(cap, monkeypatch):
-    """The cooperative choice (othello.hip coop_choose) lists only the children
-    beyond a wave's R = ceil(T / 64) rounds; a wave whose surplus exceeds the
-    overflow list falls back to per-lane evaluation for that ply.  Start every
-    game where the mover has >= 21 legal moves (mobility far above the wave's
-    mean later on), and run with the full list, a 64-entry list (some plies
-    fall back) and an empty one (OTH_COOP_CAP=0: every ply with a surplus falls
-    back): all equal the oracle."""
+    """The cooperative choice (othello.hip coop_choose) cuts the wave's T
+    children into 64 chunks of R = ceil(T / 64), found by a scan and a binary
+    search, each walking parents' masks across parent boundaries; the per-lane
+    choice (lane_choose) runs instead with OTH_COOP_CAP=0.  Start every game
+    where the mover has >= 21 legal moves (chunks that start mid-parent and
+    span several parents), both ways: all equal the oracle."""
     from subproc_amd.params import DEFAULT_WEIGHTS
     if cap is not None:
         monkeypatch.setenv("OTH_COOP_CAP", cap)

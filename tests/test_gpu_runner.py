@@ -39,8 +39,8 @@ def test_runner_fixtures(name):
 @pytest.mark.parametrize("cap", [None, "0"])
 def test_runner_vs_oracle_at_scale(policy, cap, monkeypatch):
     """8,192 matches (budgets 10 / 4, colours drawn) against the oracle, move
-    for move; with OTH_COOP_CAP=0 (2,048 matches) every ply with a choice
-    surplus takes the per-lane fallback of the cooperative choice."""
+    for move; with OTH_COOP_CAP=0 (2,048 matches) every choice is made by its
+    own lane (lane_choose) instead of the cooperative chunks."""
     if cap is not None:
         monkeypatch.setenv("OTH_COOP_CAP", cap)
     n = 8192 if cap is None else 2048

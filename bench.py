@@ -639,20 +639,24 @@ def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
 
 def _bench_td(ops, torch, dev, args, games=1 << 18):
     """§8f row 2: the learner's TD state-map update for a batch of GPU self-play
-    books (replay + ordered update stream + stable sort + per-key EMA + merge
-    into a table that already holds two batches)."""
+    books (packed replay + ordered update stream + stable sort + per-key EMA +
+    merge into a table that already holds two batches)."""
     from subproc_amd.td import StateMap
 
     rs = [ops.rollout(games, args.seed, (1 << 41) + k * games, "random", record_moves=True, device=dev)
           for k in range(3)]
     sm = StateMap(dev)
     for r in rs[:2]:  # warm-up: the empty-table path, then the merge path (first-use kernel loading)
-        sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
+        pk = ops.replay_rows(r.moves, r.plies)
+        sm.update(pk.boards, r.plies, pk.row_off)
     torch.cuda.synchronize()
     r2 = rs[2]
     t0 = time.perf_counter()
-    pos = ops.replay(r2.moves, r2.plies)
-    n_upd = sm.update(pos.boards, r2.plies)
+    # the books as GameBooks holds them: the packed replay (each game's recorded
+    # rows only), then the update over those rows (round 3 timed the strided
+    # replay, all 129 rows per game)
+    pk = ops.replay_rows(r2.moves, r2.plies)
+    n_upd = sm.update(pk.boards, r2.plies, pk.row_off)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"metric": "TD state-map updates/sec (position x side, learner order)", "value": n_upd / dt,

@@ -253,6 +253,41 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     return td_updates_any(pos_boards, row_off, plies, base, lam_pow, keys, values, n);
 }
 
+/* packed words: the same updates, OTH_TD_KEY << OTH_TD_PACK_SHIFT | (value_side + 64) << 13 | turn_left */
+int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
+                          const int64_t* base, uint64_t* words, int64_t n, void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !words))) return OTH_EINVAL;
+    for (int64_t g = 0; g < n; g++) {
+        const uint64_t* row = pos_boards + (row_off ? row_off[g] : g * OTH_POS_STRIDE) * 2;
+        const int np = plies[g] < OTH_MOVES_STRIDE ? plies[g] : OTH_MOVES_STRIDE;
+        int8_t d;
+        oracle_result(row + 2 * np, NULL, NULL, &d, NULL, 1);
+        for (int p = 0; p <= np; p++) {
+            uint8_t f[2][10];
+            const uint8_t sides[2] = {OTH_BLACK, OTH_WHITE};
+            const uint64_t b2[4] = {row[2 * p], row[2 * p + 1], row[2 * p], row[2 * p + 1]};
+            oracle_features(b2, sides, &f[0][0], 2);
+            const int64_t j = base[g] + 2 * (int64_t)(np - p);
+            const uint64_t tl = (uint64_t)(np - p);
+            words[j] = ((uint64_t)td_key(f[0]) << OTH_TD_PACK_SHIFT) | ((uint64_t)(d + 64) << 13) | tl;
+            words[j + 1] = ((uint64_t)td_key(f[1]) << OTH_TD_PACK_SHIFT) | ((uint64_t)(64 - d) << 13) | tl;
+        }
+    }
+    return OTH_OK;
+}
+
+int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
+                  void* stream) {
+    (void)stream;
+    if (n < 0 || (n > 0 && (!words || !lam_pow || !keys || !values))) return OTH_EINVAL;
+    for (int64_t i = 0; i < n; i++) {
+        keys[i] = (int64_t)(words[i] >> OTH_TD_PACK_SHIFT);
+        values[i] = (double)((int)((words[i] >> 13) & 0xffu) - 64) * lam_pow[words[i] & 0x1fffu];
+    }
+    return OTH_OK;
+}
+
 int oth_td_updates_records(const uint64_t* rows, const int64_t* term_row, const int32_t* lam_idx,
                            const double* lam_pow, int64_t* keys, double* values, int64_t n_rows, void* stream) {
     (void)stream;
@@ -333,6 +368,38 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
         keys_out[i] = keys_in[a[i]];
         vals_out[i] = vals_in[a[i]];
     }
+    return OTH_OK;
+}
+
+/* stable sort of packed words by their key bits: the pairs' merge sort over
+ * (word >> OTH_TD_PACK_SHIFT) with the words as the payload */
+int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
+                       void* stream) {
+    (void)stream;
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    const size_t need = (size_t)(n > 0 ? n : 1) * 2 * sizeof(int64_t);
+    if (!temp) {
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (*temp_bytes < need || (n > 0 && (!words_in || !words_out))) return OTH_EINVAL;
+    int64_t* a = (int64_t*)temp;
+    int64_t* b = a + n;
+    for (int64_t i = 0; i < n; i++) a[i] = i;
+    for (int64_t w = 1; w < n; w *= 2) {
+        for (int64_t lo = 0; lo < n; lo += 2 * w) {
+            const int64_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+            int64_t i = lo, j = mid, k = lo;
+            while (i < mid && j < hi)
+                b[k++] = (words_in[a[j]] >> OTH_TD_PACK_SHIFT) < (words_in[a[i]] >> OTH_TD_PACK_SHIFT) ? a[j++] : a[i++];
+            while (i < mid) b[k++] = a[i++];
+            while (j < hi) b[k++] = a[j++];
+        }
+        int64_t* t = a;
+        a = b;
+        b = t;
+    }
+    for (int64_t i = 0; i < n; i++) words_out[i] = words_in[a[i]];
     return OTH_OK;
 }
 

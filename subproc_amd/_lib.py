@@ -21,6 +21,7 @@ N_FEATURES = 10
 POLICY_RANDOM, POLICY_GREEDY, POLICY_EVAL = 0, 1, 2
 EVAL_PHASES, EVAL_FEATURES, EVAL_WEIGHTS = 4, 9, 36
 TD_KEY_BITS = 43
+TD_PACK_SHIFT = 21
 TD_FIT_BLOCKS, TD_FIT_COLS = 1024, 64
 
 # name -> (restype, argtypes); must match include/othello.h exactly
@@ -49,6 +50,9 @@ SIGNATURES = {
     "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),
     "oth_td_ema_split": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64, _P]),
     "oth_td_sort_pairs": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),
+    "oth_td_updates_packed": (_I, [_P, _P, _P, _P, _P, _I64, _P]),
+    "oth_td_sort_packed": (_I, [_P, _P, _I64, _P, _P, _P]),
+    "oth_td_unpack": (_I, [_P, _P, _P, _P, _I64, _P]),
     "oth_td_merge": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_fit_moments": (_I, [_P, _P, _I64, _P, _P, _P]),

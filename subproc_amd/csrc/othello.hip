@@ -170,19 +170,24 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
+// OTH_COOP_KEEP: the evaluator of a parent's best child hands the child's
+// boards to the parent (1), or the parent recomputes the chosen move's flips
+// (0, rounds 1-3).  OTH_COOP_PIPE: the hand-over's check of round r runs in
+// round r + 1, its LDS reads issued before that round's child is computed.
 #ifndef OTH_COOP_KEEP
 #define OTH_COOP_KEEP 1
 #endif
+#ifndef OTH_COOP_PIPE
+#define OTH_COOP_PIPE 1
+#endif
 struct CoopWave {
-    u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words)
+    u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words; A1's bit 0, a1, carries the eval table)
     u64 legal[64];    // parent lane's legal mask (0: not choosing)
 #if OTH_COOP_KEEP
     u64 win[64][2];   // the best child's boards so far: mover P2, opponent O2
-    u64 mine[64][2];  // the child this lane evaluated this round (parked across the round's sync)
+    u64 mine[64][2];  // the child this lane evaluated in the last round (parked in LDS)
 #endif
-    u32 pre[64];      // exclusive scan of the move counts
     u32 best[64];
-    uint8_t tbl[64];  // the parent's eval table (0 / 1)
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -207,8 +212,11 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 }
 // w_s: the two eval tables (kEvalTable ints each); tbl (0 / 1) is the mover's
 // (Black's / White's, or in a GameRunner match player A's / B's).  Returns
-// the chosen square of a choosing lane (64 otherwise); its child's boards are
-// left in cw.win[lane] (read them before the next call).
+// the chosen square of a choosing lane (64 otherwise); with OTH_COOP_KEEP its
+// child's boards are left in cw.win[lane] (read them before the next call).
+// The table bit rides in bit 0 (square a1) of the record's A1, the west runs
+// of inner opponent discs, which never holds a1; a stray bit 0 in A1 does not
+// change flips_col's east carry either (bit 0 of mv << 1 is 0: no carry).
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, const uint8_t* kth_tab, u32 lane, u32 cap) {
@@ -229,51 +237,81 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
     const u32 incl = wave_incl_scan(cnt);
     const u32 T = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     const u32 R = (T + 63u) >> 6;
-    cw.pre[lane] = incl - cnt;
     cw.legal[lane] = legal;
     if (need) {
         u64* r = cw.rec[lane];
         r[0] = P;
         r[1] = O;
-        *reinterpret_cast<RunSets*>(r + 2) = run_sets(pos);  // reversed once per parent, not per child
+        RunSets rs = run_sets(pos);  // reversed once per parent, not per child
+        if (POLICY == OTH_POLICY_EVAL) rs.A1 |= (u64)(tbl & 1u);
+        *reinterpret_cast<RunSets*>(r + 2) = rs;
         cw.best[lane] = 0xFFFFFFFFu;
-        if (POLICY == OTH_POLICY_EVAL) cw.tbl[lane] = (uint8_t)tbl;
     }
-    wave_sync();
-    // this lane's chunk of the children: [t0, t0 + cnt_mine)
+    // this lane's chunk of the children: [t0, t0 + cnt_mine).  Its first
+    // parent, the last lane whose first child is <= t0, by a binary search of
+    // the exclusive scan, read from the lanes' registers by permutes (every
+    // lane active); the parents with moves as one wave-uniform mask
     const u32 t0 = R * lane, cnt_mine = t0 < T ? min(R, T - t0) : 0u;
+    const u32 excl = incl - cnt;
+    const u64 with_moves = __ballot(cnt != 0);
     u32 p = 0;
+#pragma unroll
+    for (u32 step = 32; step >= 1; step >>= 1)
+        if ((u32)__shfl((int)excl, (int)(p + step)) <= t0) p += step;
+    const u32 k0 = t0 - (u32)__shfl((int)excl, (int)p);
+    wave_sync();
     u64 m = 0;
     if (cnt_mine) {
-        // the chunk's first parent: the last lane whose first child is <= t0
-#pragma unroll
-        for (u32 step = 32; step >= 1; step >>= 1)
-            if (cw.pre[p + step] <= t0) p += step;
         m = cw.legal[p];
-        const u32 k0 = t0 - cw.pre[p];  // the parent's children before the chunk
-        if (k0) m &= ~0ull << kth_bit_tab(m, k0, (u32)__popc((u32)m), kth_tab);
+        if (k0) m &= ~0ull << kth_bit_tab(m, k0, (u32)__popc((u32)m), kth_tab);  // skip the chunk's predecessors
     }
+#if OTH_COOP_KEEP && OTH_COOP_PIPE
+    u32 p_last = 0, key_last = 0xFFFFFFFFu;  // the last round's child: its parent and key
+#endif
     for (u32 r = 0; r < R; r++) {
         const bool have = r < cnt_mine;
+#if OTH_COOP_KEEP && OTH_COOP_PIPE
+        // last round's hand-over check: the reads issue now (after every lane's
+        // atomic of that round: a wave's LDS ops are in order) and are used
+        // after this round's child, which hides their latency
+        const u32 b_last = cw.best[p_last];
+        const u64 mP = cw.mine[lane][0], mO = cw.mine[lane][1];
+#endif
         u32 key = 0xFFFFFFFFu;
+        u64 cP = 0, cO = 0;
         if (have) {
-            while (m == 0) m = cw.legal[++p];  // the next parent with moves (one exists: t0 + r < T)
+            if (m == 0) {  // the next parent with moves (one exists, above p < 63: t0 + r < T)
+                p = (u32)__ffsll((unsigned long long)(with_moves & (~0ull << (p + 1)))) - 1u;
+                m = cw.legal[p];
+            }
             const u32 sq = (u32)__ffsll((unsigned long long)m) - 1u;
             m &= m - 1;
             u64 Pp, Op;
             RunSets ps;
             load_parent(cw.rec[p], Pp, Op, ps);
             const int* wt = w_s;
-            if (POLICY == OTH_POLICY_EVAL && cw.tbl[p]) wt += kEvalTable;
-            u64 cP, cO;
+            if (POLICY == OTH_POLICY_EVAL && (ps.A1 & 1ull)) wt += kEvalTable;
             key = child_key<POLICY>(Pp, Op, ps, sq, rays, wt, cP, cO);
             atomicMin(&cw.best[p], key);
-#if OTH_COOP_KEEP
-            cw.mine[lane][0] = cP;  // parked in LDS, not held in registers across the sync
-            cw.mine[lane][1] = cO;
-#endif
         }
-#if OTH_COOP_KEEP
+#if OTH_COOP_KEEP && OTH_COOP_PIPE
+        // keys are unique per parent: one writer per improved slot, and a later
+        // improvement's write comes later in the wave's LDS order
+        if (key_last != 0xFFFFFFFFu && b_last == key_last) {
+            cw.win[p_last][0] = mP;
+            cw.win[p_last][1] = mO;
+        }
+        if (have) {
+            cw.mine[lane][0] = cP;  // parked in LDS, not held in registers across the next child
+            cw.mine[lane][1] = cO;
+        }
+        p_last = p;
+        key_last = key;
+#elif OTH_COOP_KEEP
+        if (have) {
+            cw.mine[lane][0] = cP;
+            cw.mine[lane][1] = cO;
+        }
         wave_sync();  // every lane's atomic of this round before the reads (a wave's LDS ops are in order)
         if (have && cw.best[p] == key) {  // keys are unique per parent: one writer per improved slot
             cw.win[p][0] = cw.mine[lane][0];
@@ -282,6 +320,13 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
 #endif
     }
     wave_sync();
+#if OTH_COOP_KEEP && OTH_COOP_PIPE
+    if (key_last != 0xFFFFFFFFu && cw.best[p_last] == key_last) {  // the last round's hand-over
+        cw.win[p_last][0] = cw.mine[lane][0];
+        cw.win[p_last][1] = cw.mine[lane][1];
+    }
+    wave_sync();
+#endif
     return need ? cw.best[lane] & 63u : 64u;
 }
 
@@ -1431,7 +1476,7 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
                                                             const int64_t* __restrict__ base,
                                                             const double* __restrict__ lam_pow,
                                                             int64_t* __restrict__ keys, double* __restrict__ vals,
-                                                            int64_t n) {
+                                                            u64* __restrict__ words, int64_t n) {
     const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (idx >= n * OTH_POS_STRIDE) return;
     const int64_t g = idx / OTH_POS_STRIDE;
@@ -1442,8 +1487,14 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     const ulonglong2 term = row[np];
     const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
     const ulonglong2 b = row[p];
-    const double lam = lam_pow[np - p];
     const int64_t j = base[g] + 2 * (int64_t)(np - p);
+    if (words) {  // oth_td_updates_packed: (key, value_side, turn_left) in one word
+        const u64 tl = np - p;
+        words[j] = ((u64)td_key(b, OTH_BLACK) << OTH_TD_PACK_SHIFT) | ((u64)(vb + 64) << 13) | tl;
+        words[j + 1] = ((u64)td_key(b, OTH_WHITE) << OTH_TD_PACK_SHIFT) | ((u64)(64 - vb) << 13) | tl;
+        return;
+    }
+    const double lam = lam_pow[np - p];
     keys[j] = td_key(b, OTH_BLACK);
     vals[j] = (double)vb * lam;
     keys[j + 1] = td_key(b, OTH_WHITE);
@@ -2088,10 +2139,18 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
     if (n == 0) return OTH_OK;
     td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, nullptr, plies,
                                                                                           base, lam_pow, keys, values,
-                                                                                          n);
+                                                                                          nullptr, n);
     return launched();
 }
 
+int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
+                          const int64_t* base, uint64_t* words, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !words))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(
+        pos_boards, row_off, plies, base, nullptr, nullptr, nullptr, reinterpret_cast<u64*>(words), n);
+    return launched();
+}
 int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                         const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!pos_boards || !row_off || !plies || !base || !lam_pow || !keys || !values)))
@@ -2099,7 +2158,7 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     if (n == 0) return OTH_OK;
     td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, row_off, plies,
                                                                                           base, lam_pow, keys, values,
-                                                                                          n);
+                                                                                          nullptr, n);
     return launched();
 }
 

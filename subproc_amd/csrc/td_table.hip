@@ -31,6 +31,20 @@ using SortConfig = rocprim::radix_sort_config<
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 9,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
+// packed words -> (key, value): the value recomputed from the payload exactly
+// as oth_td_updates computes it
+__global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restrict__ words,
+                                                        const double* __restrict__ lam_pow,
+                                                        int64_t* __restrict__ keys, double* __restrict__ values,
+                                                        int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t w = words[i];
+    const int vs = (int)((w >> 13) & 0xffu) - 64;
+    keys[i] = (int64_t)(w >> OTH_TD_PACK_SHIFT);
+    values[i] = (double)vs * lam_pow[w & 0x1fffu];
+}
+
 constexpr int kMergeBlock = 256;
 constexpr int kMergeK = 8;                               // merged positions per thread
 constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
@@ -385,6 +399,33 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
         old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, split, out_keys, out_vals);
     e = hipGetLastError();
     return e != hipSuccess ? -(int)e : OTH_OK;
+}
+
+int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
+                       void* stream) {
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    if (!temp) {  // size query: no work, no launch
+        size_t bytes = 0;
+        const hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, bytes, words_in, words_out, (size_t)n,
+                                                                  OTH_TD_PACK_SHIFT, 64, (hipStream_t)stream);
+        *temp_bytes = bytes;
+        return e == hipSuccess ? OTH_OK : -(int)e;
+    }
+    if (n > 0 && (!words_in || !words_out)) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    size_t bytes = *temp_bytes;
+    const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
+                                                              OTH_TD_PACK_SHIFT, 64, (hipStream_t)stream);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
+                  void* stream) {
+    if (n < 0 || (n > 0 && (!words || !lam_pow || !keys || !values))) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    td_unpack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(words, lam_pow, keys, values, n);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OTH_OK : -(int)e;
 }
 
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,

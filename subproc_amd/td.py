@@ -12,11 +12,15 @@ side (progress_position_moves_learn.py:37-62):
                 v[key] = new if v[key] == 0 else v[key] * (1 - a) + new * a
 
 Here the whole batch runs on the device:
-  1. ``oth_td_updates`` (HIP) emits the ordered update stream: packed counts()
-     key + value per (position, side), from an ``oth_replay`` position table;
-  2. ``oth_td_sort_pairs`` (rocPRIM radix sort over the key's 54 bits) sorts
-     the (key, value) pairs by key, stably: each key's updates stay in stream
-     order;
+  1. ``oth_td_updates_packed`` (HIP) emits the ordered update stream from an
+     ``oth_replay`` / ``oth_replay_rows`` position table, one uint64 word per
+     (position, side): the packed counts() key, the terminal's disc
+     difference and the turns left, from which the value is recomputed
+     exactly (``oth_td_unpack``);
+  2. ``oth_td_sort_packed`` (rocPRIM keys-only radix sort over the words' 43
+     key bits) sorts them by key, stably: each key's updates stay in stream
+     order (books read from records take ``oth_td_updates_records`` and the
+     (key, value) pair sort ``oth_td_sort_pairs``);
   3. ``oth_td_ema_split`` (HIP) replays each key's updates in order in
      float64 with separate multiply and add, so every value is bit-identical
      to the Python learner's (a key with at least LONG_MIN updates gets a
@@ -148,21 +152,27 @@ class StateMap:
         ends = torch.cumsum(cnt, 0)
         base = (ends - cnt).contiguous()
         total = int(ends[-1])
-        keys = torch.empty(total, dtype=torch.int64, device=self.device)
-        vals = torch.empty(total, dtype=torch.float64, device=self.device)
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            if row_off is None:
-                check(lib.oth_td_updates(pos_boards.contiguous().data_ptr(), plies.contiguous().data_ptr(),
-                                         base.data_ptr(), self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(),
-                                         n, stream), "oth_td_updates")
-            else:
-                check(lib.oth_td_updates_rows(pos_boards.contiguous().data_ptr(), row_off.contiguous().data_ptr(),
-                                              plies.contiguous().data_ptr(), base.data_ptr(),
-                                              self._lam_pow.data_ptr(), keys.data_ptr(), vals.data_ptr(), n, stream),
-                      "oth_td_updates_rows")
-        self._apply(keys, vals)
+            # the update stream as packed words (key | value_side | turn_left), a
+            # keys-only sort of the words by their key bits (half the bytes of
+            # sorting (key, value) pairs), then keys and values back out
+            words = torch.empty(total, dtype=torch.int64, device=self.device)
+            check(lib.oth_td_updates_packed(pos_boards.contiguous().data_ptr(),
+                                            None if row_off is None else row_off.contiguous().data_ptr(),
+                                            plies.contiguous().data_ptr(), base.data_ptr(), words.data_ptr(), n,
+                                            stream), "oth_td_updates_packed")
+            sorted_words = torch.empty_like(words)
+            _with_scratch(lib.oth_td_sort_packed, (words.data_ptr(), sorted_words.data_ptr(), total), stream,
+                          self.device, "oth_td_sort_packed")
+            del words
+            sk = torch.empty(total, dtype=torch.int64, device=self.device)
+            sv = torch.empty(total, dtype=torch.float64, device=self.device)
+            check(lib.oth_td_unpack(sorted_words.data_ptr(), self._lam_pow.data_ptr(), sk.data_ptr(), sv.data_ptr(),
+                                    total, stream), "oth_td_unpack")
+            del sorted_words
+        self._apply_sorted(sk, sv)
         return total
 
     def update_from_records(self, books):
@@ -205,13 +215,16 @@ class StateMap:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
             sk, sv = torch.empty_like(keys), torch.empty_like(vals)
-            tb = ctypes.c_size_t(0)
-            check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total, None,
-                                        ctypes.byref(tb), stream), "oth_td_sort_pairs")
-            temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=self.device)
-            check(lib.oth_td_sort_pairs(keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(), total,
-                                        temp.data_ptr(), ctypes.byref(tb), stream), "oth_td_sort_pairs")
-            del temp
+            _with_scratch(lib.oth_td_sort_pairs, (keys.data_ptr(), vals.data_ptr(), sk.data_ptr(), sv.data_ptr(),
+                                                  total), stream, self.device, "oth_td_sort_pairs")
+        self._apply_sorted(sk, sv)
+
+    def _apply_sorted(self, sk, sv):
+        """The key-sorted update stream (equal keys in stream order) into the
+        table: each key's EMA in stream order, then the merge."""
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
             ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
             seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
             torch.cumsum(counts, 0, out=seg_off[1:])

@@ -96,6 +96,22 @@ def sort_pair(keys, vals, keys_out, vals_out, n):
 
 
 @pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
+def test_td_sort_packed_stable(n, distinct):
+    """Packed words with keys over all OTH_TD_KEY_BITS bits and many repeats,
+    the payload bits a stream position: both builds sort by the key bits
+    alone, stably, the payload riding along."""
+    rng = np.random.default_rng(n + 1)
+    pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
+    pool[0], pool[-1] = 0, (1 << _lib.TD_KEY_BITS) - 1
+    k = pool[rng.integers(0, distinct, size=n)].astype(np.uint64)
+    w = (k << np.uint64(_lib.TD_PACK_SHIFT)) | (np.arange(n, dtype=np.uint64) & np.uint64((1 << _lib.TD_PACK_SHIFT) - 1))
+    words, out = Buf(w), Buf(np.zeros(n, np.uint64))
+    both_scratch("oth_td_sort_packed", words, out, n)
+    same(out)
+    np.testing.assert_array_equal(out.h, w[np.argsort(k, kind="stable")])
+
+
+@pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
 def test_td_sort_pairs_stable(n, distinct):
     """Keys over all OTH_TD_KEY_BITS key bits with many repeats: both builds sort
     stably (values are the stream positions, so any reordering of equal keys shows)."""
@@ -340,6 +356,22 @@ def test_td_pair():
     sort_pair(keys, vals, sk2, sv2, total)
     np.testing.assert_array_equal(sk2.h, keys.h[order])
     np.testing.assert_array_equal(sv2.h.view(np.int64), sv.h.view(np.int64))
+    # the packed path (StateMap.update): the same stream as words, sorted by
+    # their key bits with the payload riding along, unpacked -> the same
+    # sorted keys and values, bit for bit, on both builds and both layouts
+    for po, layout in ((None, pos), (off, prow)):
+        words = Buf(np.zeros(total, np.uint64))
+        both("oth_td_updates_packed", layout, po, plies, base, words, n)
+        same(words)
+        np.testing.assert_array_equal((words.h >> np.uint64(_lib.TD_PACK_SHIFT)).astype(np.int64), keys.h)
+        sw = Buf(np.zeros(total, np.uint64))
+        both_scratch("oth_td_sort_packed", words, sw, total)
+        same(sw)
+        uk2, uv2 = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+        both("oth_td_unpack", sw, lam, uk2, uv2, total)
+        same(uk2, uv2)
+        np.testing.assert_array_equal(uk2.h, keys.h[order])
+        np.testing.assert_array_equal(uv2.h.view(np.int64), sv.h.view(np.int64))
     seg = Buf(np.append(starts, total).astype(np.int64))
     init = Buf(np.random.default_rng(4).choice([0.0, 0.5, -1.25], len(uk)))
     out = Buf(np.zeros(len(uk), np.float64))

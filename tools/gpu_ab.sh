@@ -3,8 +3,12 @@
 # the step builds (if present), and a kernel trace of the TD state-map update
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-ab}; mkdir -p $O
-if [ -f build/var/keep1.so ]; then
-  timeout -k 10 400 python tools/diag/policy_ab.py build/var/r03coop.so build/var/keep1.so build/var/keep0.so --policies greedy,eval --reps 5 > $O/coop_ab.log 2>&1 || { cat $O/coop_ab.log; exit 1; }
+if [ -n "$TESTS" ]; then
+  timeout -k 10 500 python -u -m pytest $TESTS -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tail -2 $O/pytest.log
+fi
+if [ -f build/var/pipe.so ]; then
+  timeout -k 10 400 python tools/diag/policy_ab.py build/var/r03coop.so build/var/pipe.so build/var/nopipe.so build/var/keep0.so --policies greedy,eval --reps 5 > $O/coop_ab.log 2>&1 || { cat $O/coop_ab.log; exit 1; }
   cat $O/coop_ab.log
 fi
 if [ -f build/var/step_k1.so ]; then

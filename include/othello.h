@@ -307,22 +307,23 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 /* Packed updates (the GPU books' path, StateMap.update): the update stream
  * of oth_td_updates / oth_td_updates_rows (row_off NULL: the strided table)
  * with each update as one uint64 word,
- *   OTH_TD_KEY << OTH_TD_PACK_SHIFT | (value_side + 64) << 13 | turn_left,
+ *   (value_side + 64) << 56 | turn_left << 43 | OTH_TD_KEY,
  * turn_left = plies[g] - p (0..128), value_side = +-(n_black - n_white) of
  * the terminal: the value is value_side * lam_pow[turn_left], exactly the
  * double oth_td_updates writes, and oth_td_unpack recomputes it.  Half the
  * bytes of a (key, value) pair, and the grouping sort becomes a keys-only
- * sort of these words by their key bits (oth_td_sort_packed): the payload
- * rides along in the word. */
-#define OTH_TD_PACK_SHIFT 21
+ * sort of these words by their low OTH_TD_KEY_BITS (oth_td_sort_packed):
+ * the payload rides along in the word's top bits. */
+#define OTH_TD_PACK_TURN_SHIFT 43
+#define OTH_TD_PACK_VALUE_SHIFT 56
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream);
-/* Stable sort of n packed words by bits OTH_TD_PACK_SHIFT..63 (the key):
+/* Stable sort of n packed words by bits 0..OTH_TD_KEY_BITS-1 (the key):
  * equal keys keep their stream order.  temp / temp_bytes as
  * oth_td_sort_pairs. */
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream);
-/* Packed words -> keys[i] = word >> OTH_TD_PACK_SHIFT and values[i] =
+/* Packed words -> keys[i] = the word's low OTH_TD_KEY_BITS and values[i] =
  * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device). */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                   void* stream);

@@ -253,7 +253,7 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     return td_updates_any(pos_boards, row_off, plies, base, lam_pow, keys, values, n);
 }
 
-/* packed words: the same updates, OTH_TD_KEY << OTH_TD_PACK_SHIFT | (value_side + 64) << 13 | turn_left */
+/* packed words: the same updates, (value_side + 64) << 56 | turn_left << 43 | OTH_TD_KEY */
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream) {
     (void)stream;
@@ -270,8 +270,9 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
             oracle_features(b2, sides, &f[0][0], 2);
             const int64_t j = base[g] + 2 * (int64_t)(np - p);
             const uint64_t tl = (uint64_t)(np - p);
-            words[j] = ((uint64_t)td_key(f[0]) << OTH_TD_PACK_SHIFT) | ((uint64_t)(d + 64) << 13) | tl;
-            words[j + 1] = ((uint64_t)td_key(f[1]) << OTH_TD_PACK_SHIFT) | ((uint64_t)(64 - d) << 13) | tl;
+            const uint64_t t = tl << OTH_TD_PACK_TURN_SHIFT;
+            words[j] = ((uint64_t)(d + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (uint64_t)td_key(f[0]);
+            words[j + 1] = ((uint64_t)(64 - d) << OTH_TD_PACK_VALUE_SHIFT) | t | (uint64_t)td_key(f[1]);
         }
     }
     return OTH_OK;
@@ -282,8 +283,9 @@ int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, d
     (void)stream;
     if (n < 0 || (n > 0 && (!words || !lam_pow || !keys || !values))) return OTH_EINVAL;
     for (int64_t i = 0; i < n; i++) {
-        keys[i] = (int64_t)(words[i] >> OTH_TD_PACK_SHIFT);
-        values[i] = (double)((int)((words[i] >> 13) & 0xffu) - 64) * lam_pow[words[i] & 0x1fffu];
+        keys[i] = (int64_t)(words[i] & ((1ull << OTH_TD_KEY_BITS) - 1));
+        values[i] = (double)((int)(words[i] >> OTH_TD_PACK_VALUE_SHIFT) - 64) *
+                    lam_pow[(words[i] >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
     }
     return OTH_OK;
 }
@@ -372,7 +374,8 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
 }
 
 /* stable sort of packed words by their key bits: the pairs' merge sort over
- * (word >> OTH_TD_PACK_SHIFT) with the words as the payload */
+ * the words' low OTH_TD_KEY_BITS with the words as the payload */
+#define KEY_MASK ((1ull << OTH_TD_KEY_BITS) - 1)
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream) {
     (void)stream;
@@ -391,7 +394,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
             const int64_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
             int64_t i = lo, j = mid, k = lo;
             while (i < mid && j < hi)
-                b[k++] = (words_in[a[j]] >> OTH_TD_PACK_SHIFT) < (words_in[a[i]] >> OTH_TD_PACK_SHIFT) ? a[j++] : a[i++];
+                b[k++] = (words_in[a[j]] & KEY_MASK) < (words_in[a[i]] & KEY_MASK) ? a[j++] : a[i++];
             while (i < mid) b[k++] = a[i++];
             while (j < hi) b[k++] = a[j++];
         }

@@ -1490,8 +1490,9 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     const int64_t j = base[g] + 2 * (int64_t)(np - p);
     if (words) {  // oth_td_updates_packed: (key, value_side, turn_left) in one word
         const u64 tl = np - p;
-        words[j] = ((u64)td_key(b, OTH_BLACK) << OTH_TD_PACK_SHIFT) | ((u64)(vb + 64) << 13) | tl;
-        words[j + 1] = ((u64)td_key(b, OTH_WHITE) << OTH_TD_PACK_SHIFT) | ((u64)(64 - vb) << 13) | tl;
+        const u64 t = tl << OTH_TD_PACK_TURN_SHIFT;
+        words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_BLACK);
+        words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_WHITE);
         return;
     }
     const double lam = lam_pow[np - p];

@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t w = words[i];
-    const int vs = (int)((w >> 13) & 0xffu) - 64;
-    keys[i] = (int64_t)(w >> OTH_TD_PACK_SHIFT);
-    values[i] = (double)vs * lam_pow[w & 0x1fffu];
+    const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
+    keys[i] = (int64_t)(w & ((1ull << OTH_TD_KEY_BITS) - 1));
+    values[i] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
 }
 
 constexpr int kMergeBlock = 256;
@@ -407,7 +407,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     if (!temp) {  // size query: no work, no launch
         size_t bytes = 0;
         const hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, bytes, words_in, words_out, (size_t)n,
-                                                                  OTH_TD_PACK_SHIFT, 64, (hipStream_t)stream);
+                                                                  0, OTH_TD_KEY_BITS, (hipStream_t)stream);
         *temp_bytes = bytes;
         return e == hipSuccess ? OTH_OK : -(int)e;
     }
@@ -415,7 +415,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     if (n == 0) return OTH_OK;
     size_t bytes = *temp_bytes;
     const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
-                                                              OTH_TD_PACK_SHIFT, 64, (hipStream_t)stream);
+                                                              0, OTH_TD_KEY_BITS, (hipStream_t)stream);
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 

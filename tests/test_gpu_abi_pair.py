@@ -98,13 +98,13 @@ def sort_pair(keys, vals, keys_out, vals_out, n):
 @pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
 def test_td_sort_packed_stable(n, distinct):
     """Packed words with keys over all OTH_TD_KEY_BITS bits and many repeats,
-    the payload bits a stream position: both builds sort by the key bits
-    alone, stably, the payload riding along."""
+    the payload bits (the top 21) a stream position: both builds sort by the
+    key bits alone, stably, the payload riding along."""
     rng = np.random.default_rng(n + 1)
     pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
     pool[0], pool[-1] = 0, (1 << _lib.TD_KEY_BITS) - 1
     k = pool[rng.integers(0, distinct, size=n)].astype(np.uint64)
-    w = (k << np.uint64(_lib.TD_PACK_SHIFT)) | (np.arange(n, dtype=np.uint64) & np.uint64((1 << _lib.TD_PACK_SHIFT) - 1))
+    w = (np.arange(n, dtype=np.uint64) << np.uint64(_lib.TD_KEY_BITS)) | k  # the payload: stream positions
     words, out = Buf(w), Buf(np.zeros(n, np.uint64))
     both_scratch("oth_td_sort_packed", words, out, n)
     same(out)
@@ -363,7 +363,7 @@ def test_td_pair():
         words = Buf(np.zeros(total, np.uint64))
         both("oth_td_updates_packed", layout, po, plies, base, words, n)
         same(words)
-        np.testing.assert_array_equal((words.h >> np.uint64(_lib.TD_PACK_SHIFT)).astype(np.int64), keys.h)
+        np.testing.assert_array_equal((words.h & np.uint64((1 << _lib.TD_KEY_BITS) - 1)).astype(np.int64), keys.h)
         sw = Buf(np.zeros(total, np.uint64))
         both_scratch("oth_td_sort_packed", words, sw, total)
         same(sw)

@@ -541,17 +541,29 @@ def _bench_sharded(torch, args, policy, steps=10, reps=3):
     n = args.games
     rollout_sharded(2 * n, args.seed, policy, steps=2, game_id_base=1 << 45)  # first-use warm-up
     torch.cuda.synchronize()
-    rates = []
-    for r in range(reps):
-        t0 = time.perf_counter()
-        hist, _ = rollout_sharded(steps * n, args.seed, policy, steps=steps, game_id_base=(1 << 45) + (r + 1) * steps * n)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        rates.append(int(hist[132]) / dt)
-    rates.sort()
-    return {"metric": "env-steps/sec (dist.rollout_sharded, %d pipelined launches of %d games, one process)"
-                      % (steps, n), "value": rates[len(rates) // 2], "unit": "env-steps/s", "reps": rates,
-            "policy": policy}
+    out = {"metric": "env-steps/sec (dist.rollout_sharded, %d pipelined launches of %d games, one process)"
+                     % (steps, n), "unit": "env-steps/s", "policy": policy}
+    for streams in (2, 3):
+        rates, gpu_rates = [], []
+        for r in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            hist, _ = rollout_sharded(steps * n, args.seed, policy, steps=steps, streams=streams,
+                                      game_id_base=(1 << 45) + (r + 1) * steps * n)
+            e1.record()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            env = int(hist[132])
+            rates.append(env / dt)  # the caller's clock: Python set-up and the last launch's tail included
+            gpu_rates.append(env / (e0.elapsed_time(e1) * 1e-3))  # the stream's clock, call entry to last launch end
+        rates.sort()
+        gpu_rates.sort()
+        key = "" if streams == 2 else "_3streams"
+        out["value" + key] = rates[len(rates) // 2]
+        out["gpu_clock_value" + key] = gpu_rates[len(gpu_rates) // 2]
+        out["reps" + key] = rates
+    return out
 
 
 def _bench_rollout_big(ops, torch, dev, args, games=1 << 24, reps=3):

@@ -231,7 +231,8 @@ def main():
             what = "greedy-mobility" if pol == "greedy" else "linear-eval (learner default weights)"
             return {"metric": f"env-steps/sec ({what} self-play)", "value": r["value"], "unit": r["unit"],
                     "games": args.games, "steps": a.steps, "streams": args.streams, "ms_per_step": r["ms_per_step"],
-                    "launch_ms": r["roofline"]["launch_ms"], "valu": r.get("valu")}
+                    "launch_ms": r["roofline"]["launch_ms"], "valu": r.get("valu"),
+                    "grid_blocks": r["config"]["grid_blocks"], "cus": r["config"]["cus"]}
 
         if args.workload != "greedy":
             guarded("greedy_1M", lambda: policy_line("greedy"))
@@ -410,6 +411,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
                        ({"random": "3" if world == 1 else "4", "greedy": "5", "eval": " §8f"}[policy], policy),
                        "games_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
                        "streams": nstreams, "env_steps_per_game": env_steps / games, "world_size": world,
+                       "grid_blocks": lib.oth_rollout_grid(pid, n),
+                       "cus": torch.cuda.get_device_properties(dev).multi_processor_count,
                        "game_ids": _game_id_ranges(n, world, args.warmup, args.steps),
                        "games_counted": counted, "env_steps": env_steps,
                        "black_white_draw": [int(v) for v in timed[129:132]]})

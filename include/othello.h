@@ -138,6 +138,12 @@ int oth_rollout(const uint64_t* start, const uint8_t* start_turn, uint64_t seed,
                 int policy, int n_random, uint64_t* final_boards, int8_t* diff, uint8_t* plies,
                 uint8_t* moves, int64_t* hist, uint64_t* work, int64_t n, void* stream);
 
+/* Launch geometry (diagnostic, no launch): the number of 256-thread blocks a
+ * rollout of n games with `policy` launches on the current device -- its
+ * resident-block count, at most one block per 256 games -- or OTH_EINVAL for
+ * an unknown policy.  The CPU build returns 1. */
+int oth_rollout_grid(int policy, int64_t n);
+
 /* oth_rollout with the eval policy: after n_random random plies, each mover
  * plays the legal move whose child maximises oth_eval(child, mover) under
  * `weights` (HOST pointer to OTH_EVAL_WEIGHTS int8, copied into the launch, so

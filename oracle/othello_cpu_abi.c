@@ -238,6 +238,11 @@ static int td_updates_any(const uint64_t* pos_boards, const int64_t* row_off, co
     return OTH_OK;
 }
 
+int oth_rollout_grid(int policy, int64_t n) {
+    if (n < 0 || policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_EVAL) return OTH_EINVAL;
+    return 1;
+}
+
 int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64_t* base, const double* lam_pow,
                    int64_t* keys, double* values, int64_t n, void* stream) {
     (void)stream;

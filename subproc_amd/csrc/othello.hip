@@ -2221,6 +2221,16 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     return launched();
 }
 
+int oth_rollout_grid(int policy, int64_t n) {
+    if (n < 0 || policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_EVAL) return OTH_EINVAL;
+    DeviceState* ds = device_state();
+    if (!ds) return status(hipErrorInvalidDevice);
+    const Tuning& t = ds->tuning;
+    const unsigned resident =
+        policy == OTH_POLICY_RANDOM && n >= kBigLaunch ? t.random_big_blocks : t.resident_blocks[policy];
+    return (int)std::min<int64_t>((n + kBlock - 1) / kBlock, (int64_t)resident);
+}
+
 int oth_sample_midgame(uint64_t seed, uint64_t index0, uint64_t* boards, uint8_t* turn, uint8_t* nturn,
                        uint8_t* move, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!boards || !turn || !move))) return OTH_EINVAL;

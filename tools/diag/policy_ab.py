@@ -71,9 +71,13 @@ for pol in a.policies.split(","):
             e1.record(st)
             torch.cuda.synchronize()
             times[i].append((e0.elapsed_time(e1), int(h[132])))
-    for path, t in zip(a.libs, times):
+    for path, L, t in zip(a.libs, libs, times):
+        grid = "?"
+        if hasattr(L, "oth_rollout_grid"):
+            L.oth_rollout_grid.restype, L.oth_rollout_grid.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_int64]
+            grid = L.oth_rollout_grid({"random": 0, "greedy": 1, "eval": 2}[pol], n)
         ms = sorted(x[0] for x in t)
         med = ms[len(ms) // 2]
         steps = sum(x[1] for x in t) / len(t)
-        print("%-8s %-28s median %.3f ms  min %.3f  %.3e env-steps/s" % (pol, os.path.basename(path), med, ms[0],
-                                                                       steps / med * 1e3), flush=True)
+        print("%-8s %-28s median %.3f ms  min %.3f  %.3e env-steps/s  grid %s blocks" % (
+            pol, os.path.basename(path), med, ms[0], steps / med * 1e3, grid), flush=True)

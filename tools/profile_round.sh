@@ -11,9 +11,9 @@ mkdir -p $O
 # no time-based pre-warm (single-stream launches) in profiled runs: every launch of
 # the headline kernel is then a two-stream bench step, as in the bench line
 BENCH="bench.py --steps 100 --warmup 100 --prewarm-ms 0"
-# rollout_16M and rollout_1stream share the headline kernel and grid: keep them
+# rollout_16M, rollout_1stream and rollout_sharded share the headline kernel and grid: keep them
 # out of the per-launch averages
-export BENCH_SKIP=rollout_16M,rollout_1stream
+export BENCH_SKIP=rollout_16M,rollout_1stream,rollout_sharded
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $BENCH > $O/kt_bench.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $BENCH > $O/fetch.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $BENCH > $O/write.log 2>&1 || exit 1

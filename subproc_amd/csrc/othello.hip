@@ -108,45 +108,45 @@ __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
 // 1-ply policies (greedy: minimise the opponent's mobility on the child; eval:
 // maximise the mover's linear eval of the child; ties -> lowest square, the
 // first in puttables order).  A child's score is a key whose minimum is the
-// choice: (score << 6) | square.  The child's boards (mover P2, opponent O2)
-// come back too: the chosen child is the next position, so the choice needs
-// no second flip computation.
+// choice: (score << 6) | square.  The parent then plays the chosen square
+// itself (one flip computation): handing the best child's boards over through
+// LDS instead cost more than it saved (round 4 A/B on one box, 1,048,576 games:
+// greedy 2.245 / 2.226 ms with the hand-over, pipelined or not, against
+// 2.183 ms without; eval 4.123 / 4.364 against 3.960 ms).
+//
+// the eval weight row of a parent's children: every child has popcount(P|O) + 1
+// discs, so one row serves all of them (its address found once per parent;
+// the weights themselves are read per child: held in registers they pushed
+// the eval kernel past its 128 VGPRs)
 template <int POLICY>
-__device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* w_tab,
-                                         u64& P2, u64& O2) {
-    P2 = P;
-    O2 = O;
-    place(P2, O2, flips_rays(sq, s, rays));
-    if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O2, P2)) << 6) | sq;
-    // every child has popcount(P|O) + 1 discs: one weight row per parent
-    const int* row = w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
+__device__ __forceinline__ const int* child_row(u64 P, u64 O, const int* w_tab) {
+    if (POLICY != OTH_POLICY_EVAL) return w_tab;
+    return w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
+}
+template <int POLICY>
+__device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* row) {
+    place(P, O, flips_rays(sq, s, rays));
+    if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O, P)) << 6) | sq;
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
     // |v| < 2^14; fill order 7-9-8 (bitboard.hpp analyse): 9 same-bank v_bitop3_b32 in
     // this child loop against 13 at 8-7-9, +2-4% eval env-steps/s (tools/diag/r03_evalorder.sh)
-    const int v = eval_linear(w, P2, moves<798>(P2, O2));
+    const int v = eval_linear(w, P, moves<798>(P, O));
     return ((u32)((1 << 20) - v) << 6) | sq;
 }
 
-// one lane alone over its own children (w_tab: the mover's eval table); the
-// chosen child's boards into P2 / O2
+// one lane alone over its own children (w_tab: the mover's eval table)
 template <int POLICY>
-__device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, const u64* rays, const int* w_tab,
-                                           u64& P2, u64& O2) {
+__device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, const u64* rays, const int* w_tab) {
     u32 best = 0xFFFFFFFFu;
     u64 legal = pos.legal;
     const RunSets s = run_sets(pos);
+    const int* row = child_row<POLICY>(P, O, w_tab);
     while (legal) {
         const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
         legal &= legal - 1;
-        u64 cP, cO;
-        const u32 k = child_key<POLICY>(P, O, s, sq, rays, w_tab, cP, cO);
-        if (k < best) {
-            best = k;
-            P2 = cP;
-            O2 = cO;
-        }
+        best = min(best, child_key<POLICY>(P, O, s, sq, rays, row));
     }
     return best & 63u;
 }
@@ -158,35 +158,24 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // the lanes' move counts), are cut into 64 consecutive chunks of
 // R = ceil(T / 64): lane i evaluates children R*i .. R*i + R - 1 in R rounds
 // (finished games included).  A lane finds its chunk's first parent by a
-// binary search of the scan in LDS and skips that parent's first children by
-// the k-th-bit pick; from there it walks the parents' legal masks lowest
-// square first, moving to the next parent with moves when one runs out.
-// Every choosing lane publishes its position (P, O, run sets) and legal mask
-// to the wave's LDS area; each child's key is folded into its parent's slot
-// with an LDS atomicMin (the order of evaluation does not matter), and the
-// evaluator whose key is the slot's minimum after its round writes the
-// child's boards to the parent's slot: the parent takes its next position
-// from there.  (Round 3 listed each lane's surplus children in an overflow
+// binary search of the scan and skips that parent's first children by the
+// k-th-bit pick; from there it walks the parents' legal masks lowest square
+// first, moving to the next parent with moves when one runs out.  A chunk
+// spans one or two parents mostly, so the lane holds its current parent's
+// record (and eval weight row) in registers and reads the next one from LDS
+// only when it moves on.  Every choosing lane publishes its position (P, O,
+// run sets) and legal mask to the wave's LDS area; each child's key is folded
+// into its parent's slot with an LDS atomicMin (the order of evaluation does
+// not matter).  (Round 3 listed each lane's surplus children in an overflow
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
-// OTH_COOP_KEEP: the evaluator of a parent's best child hands the child's
-// boards to the parent (1), or the parent recomputes the chosen move's flips
-// (0, rounds 1-3).  OTH_COOP_PIPE: the hand-over's check of round r runs in
-// round r + 1, its LDS reads issued before that round's child is computed.
-#ifndef OTH_COOP_KEEP
-#define OTH_COOP_KEEP 1
-#endif
-#ifndef OTH_COOP_PIPE
-#define OTH_COOP_PIPE 1
+#ifndef OTH_COOP_HOLD_EVAL  // A/B builds only (tools/gpu_ab.sh)
+#define OTH_COOP_HOLD_EVAL 0
 #endif
 struct CoopWave {
     u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words; A1's bit 0, a1, carries the eval table)
     u64 legal[64];    // parent lane's legal mask (0: not choosing)
-#if OTH_COOP_KEEP
-    u64 win[64][2];   // the best child's boards so far: mover P2, opponent O2
-    u64 mine[64][2];  // the child this lane evaluated in the last round (parked in LDS)
-#endif
     u32 best[64];
 };
 __device__ __forceinline__ void wave_sync() {
@@ -212,26 +201,14 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 }
 // w_s: the two eval tables (kEvalTable ints each); tbl (0 / 1) is the mover's
 // (Black's / White's, or in a GameRunner match player A's / B's).  Returns
-// the chosen square of a choosing lane (64 otherwise); with OTH_COOP_KEEP its
-// child's boards are left in cw.win[lane] (read them before the next call).
+// the chosen square of a choosing lane (64 otherwise).
 // The table bit rides in bit 0 (square a1) of the record's A1, the west runs
 // of inner opponent discs, which never holds a1; a stray bit 0 in A1 does not
 // change flips_col's east carry either (bit 0 of mv << 1 is 0: no carry).
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, const uint8_t* kth_tab, u32 lane, u32 cap) {
-    if (cap == 0) {
-        u32 result = 64;
-        if (need) {
-            u64 P2, O2;
-            result = lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0), P2, O2);
-#if OTH_COOP_KEEP
-            cw.win[lane][0] = P2;
-            cw.win[lane][1] = O2;
-#endif
-        }
-        return result;
-    }
+    if (cap == 0) return need ? lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0)) : 64u;
     const u64 legal = need ? pos.legal : 0ull;
     const u32 cnt = (u32)__popcll(legal);
     const u32 incl = wave_incl_scan(cnt);
@@ -260,73 +237,34 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
         if ((u32)__shfl((int)excl, (int)(p + step)) <= t0) p += step;
     const u32 k0 = t0 - (u32)__shfl((int)excl, (int)p);
     wave_sync();
-    u64 m = 0;
+    // the current parent: its remaining squares m, its record and weight row
+    // (greedy holds the record across its children; eval, at its 128 VGPRs,
+    // rereads it per child: held, it spilled)
+    constexpr bool kHold = POLICY != OTH_POLICY_EVAL || OTH_COOP_HOLD_EVAL;
+    u64 m = 0, Pp = 0, Op = 0;
+    RunSets ps = {};
+    const int* row = w_s;
+    auto enter = [&](u32 q) {
+        load_parent(cw.rec[q], Pp, Op, ps);
+        row = child_row<POLICY>(Pp, Op, w_s + ((ps.A1 & 1ull) ? kEvalTable : 0));
+    };
     if (cnt_mine) {
         m = cw.legal[p];
+        if (kHold) enter(p);
         if (k0) m &= ~0ull << kth_bit_tab(m, k0, (u32)__popc((u32)m), kth_tab);  // skip the chunk's predecessors
     }
-#if OTH_COOP_KEEP && OTH_COOP_PIPE
-    u32 p_last = 0, key_last = 0xFFFFFFFFu;  // the last round's child: its parent and key
-#endif
-    for (u32 r = 0; r < R; r++) {
-        const bool have = r < cnt_mine;
-#if OTH_COOP_KEEP && OTH_COOP_PIPE
-        // last round's hand-over check: the reads issue now (after every lane's
-        // atomic of that round: a wave's LDS ops are in order) and are used
-        // after this round's child, which hides their latency
-        const u32 b_last = cw.best[p_last];
-        const u64 mP = cw.mine[lane][0], mO = cw.mine[lane][1];
-#endif
-        u32 key = 0xFFFFFFFFu;
-        u64 cP = 0, cO = 0;
-        if (have) {
-            if (m == 0) {  // the next parent with moves (one exists, above p < 63: t0 + r < T)
-                p = (u32)__ffsll((unsigned long long)(with_moves & (~0ull << (p + 1)))) - 1u;
-                m = cw.legal[p];
-            }
-            const u32 sq = (u32)__ffsll((unsigned long long)m) - 1u;
-            m &= m - 1;
-            u64 Pp, Op;
-            RunSets ps;
-            load_parent(cw.rec[p], Pp, Op, ps);
-            const int* wt = w_s;
-            if (POLICY == OTH_POLICY_EVAL && (ps.A1 & 1ull)) wt += kEvalTable;
-            key = child_key<POLICY>(Pp, Op, ps, sq, rays, wt, cP, cO);
-            atomicMin(&cw.best[p], key);
+    for (u32 r = 0; r < cnt_mine; r++) {
+        if (m == 0) {  // the next parent with moves (one exists, above p < 63: t0 + r < T)
+            p = (u32)__ffsll((unsigned long long)(with_moves & (~0ull << (p + 1)))) - 1u;
+            m = cw.legal[p];
+            if (kHold) enter(p);
         }
-#if OTH_COOP_KEEP && OTH_COOP_PIPE
-        // keys are unique per parent: one writer per improved slot, and a later
-        // improvement's write comes later in the wave's LDS order
-        if (key_last != 0xFFFFFFFFu && b_last == key_last) {
-            cw.win[p_last][0] = mP;
-            cw.win[p_last][1] = mO;
-        }
-        if (have) {
-            cw.mine[lane][0] = cP;  // parked in LDS, not held in registers across the next child
-            cw.mine[lane][1] = cO;
-        }
-        p_last = p;
-        key_last = key;
-#elif OTH_COOP_KEEP
-        if (have) {
-            cw.mine[lane][0] = cP;
-            cw.mine[lane][1] = cO;
-        }
-        wave_sync();  // every lane's atomic of this round before the reads (a wave's LDS ops are in order)
-        if (have && cw.best[p] == key) {  // keys are unique per parent: one writer per improved slot
-            cw.win[p][0] = cw.mine[lane][0];
-            cw.win[p][1] = cw.mine[lane][1];
-        }
-#endif
+        if (!kHold) enter(p);
+        const u32 sq = (u32)__ffsll((unsigned long long)m) - 1u;
+        m &= m - 1;
+        atomicMin(&cw.best[p], child_key<POLICY>(Pp, Op, ps, sq, rays, row));
     }
     wave_sync();
-#if OTH_COOP_KEEP && OTH_COOP_PIPE
-    if (key_last != 0xFFFFFFFFu && cw.best[p_last] == key_last) {  // the last round's hand-over
-        cw.win[p_last][0] = cw.mine[lane][0];
-        cw.win[p_last][1] = cw.mine[lane][1];
-    }
-    wave_sync();
-#endif
     return need ? cw.best[lane] & 63u : 64u;
 }
 
@@ -844,15 +782,7 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 }
                 if (moving) {
                     if (RECORD) rec_put(ply, (uint8_t)sq);
-#if OTH_COOP_KEEP
-                    if (choose) {  // the child the choice evaluated is the next position (the
-                        P = cw.win[lane][0];  // slot is rewritten only by the next ply's choice)
-                        O = cw.win[lane][1];
-                    } else  // a random move (the first plies, or go_for's coin)
-#endif
-                    {
-                        place(P, O, flips_rays(sq, run_sets(pos), rays));
-                    }
+                    place(P, O, flips_rays(sq, run_sets(pos), rays));
                     const u64 np = O;
                     O = P;
                     P = np;
@@ -1626,120 +1556,184 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
 // over up to kSpecParts lanes of one block.  The rule is a contraction
 // (|1 - a| < 1): two runs over the same values from different states approach
 // each other by |1 - a| per step and, once a rounding maps them to the same
-// double, stay equal.  So the lane of part p > 0 guesses the state at the
-// start of its part by a warm-up run over the `warm` values before it, from
-// state 0 (the rule then starts at the first value itself), or exactly, from
-// the key's initial state, when the part starts within `warm` of the segment;
-// `warm` is sized by the launcher so that |1 - a|^warm < 2^-64.  Lane p then
-// runs its part from the guess.  If every part's guess equals the end state
-// of the part before (checked by all lanes at once), every part ran from the
-// exact state and the last part's end is the sequential result; otherwise
-// lane 0 walks the parts in order and reruns those whose guess missed from
-// the verified state.  Every result is thus the sequential one; speculation
-// only decides how fast it comes.
-// A lane's chain is bound by the loads it keeps in flight (each lane streams
-// its own range): round 3 ran 64 parts per key of >= 2 * warm values each
-// with 48 loads in flight per lane, 5,500 steps for the opening key at ~70
-// ns each, and one launch per batch took 376-951 us (profiles/
-// r03_profile_summary.json).  Here parts are ~kSpecPart values (up to 256 of
-// them, 4 waves), so no lane runs more than kSpecPart + warm (~2,500) steps,
-// and each lane keeps kSpecRing chunks (80 values) in flight (6 would pass the
-// 256 architectural VGPRs into AGPRs).
-constexpr int kSpecParts = 256;   // lanes per block: parts of one key, at most
-constexpr int kSpecPart = 1024;   // values per part (fewer parts for shorter keys)
-constexpr int kSpecRing = 5;      // chunks of kTdChunk values in flight per lane
-// the rule over vals[i, e) from state v, one lane, kSpecRing chunks ahead
-__device__ __forceinline__ double td_range_deep(double v, const double* __restrict__ vals, int64_t i, const int64_t e,
-                                                double a, double oma) {
-    constexpr int W = kSpecRing * kTdChunk;
-    if (e - i < W) {
-        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
-        return v;
-    }
-    const int64_t last = e - 1;
-    double buf[kSpecRing][kTdChunk];
-#pragma unroll
-    for (int c = 0; c < kSpecRing; c++) td_load(buf[c], vals, i + c * kTdChunk, last);
-    for (; i + W <= e; i += W) {
-#pragma unroll
-        for (int c = 0; c < kSpecRing; c++) {
-            v = td_run_full(v, buf[c], a, oma);
-            td_load(buf[c], vals, i + W + c * kTdChunk, last);  // kSpecRing chunks ahead (clamped)
-        }
-    }
-    const int r = (int)(e - i);  // 0 .. W-1 values left, already in buf
-#pragma unroll
-    for (int c = 0; c < kSpecRing; c++) v = td_run(v, buf[c], r - c * kTdChunk, a, oma);
-    return v;
+// double, mostly stay equal.  So the lane of part p > 0 guesses the state at
+// the start of its part by a warm-up run over the `warm` values before it,
+// from state 0 (the rule then starts at the first value itself), or exactly,
+// from the key's initial state, when the part starts within `warm` of the
+// segment; `warm` is sized by the launcher so that |1 - a|^warm < 2^-64.
+// Lane p then runs its part from the guess.  A part whose guess equals the
+// end state of the part before, itself exact, ran from the exact state; part
+// 0 is exact.  The guesses that missed (the last ulp had not merged yet: ~1 in
+// 1,000 parts, tools/diag/td_spec_probe.py) are rerun by their lanes in
+// parallel from the end state of the part before, and the check repeats until
+// every part matches its predecessor; each pass fixes at least the first
+// miss.  Every result is thus the sequential one; speculation only decides
+// how fast it comes.
+// Feeding the lanes: each lane streams its own range, so a lane-private load
+// touches 64 cache lines per wave instruction (round 4's first version: 1,024
+// line lookups per wave per 16 steps, 486-676 us per launch at ~190 ns a
+// step).  Here the block moves its parts' values in rounds of kTdChunk per
+// lane: the threads load the round's parts x 16 doubles cooperatively (a wave
+// instruction covers 4 rows of 16 consecutive doubles: 4-8 lines) through a
+// buffer descriptor that advances 16 doubles a round (fixed per-lane offsets,
+// no address arithmetic; the descriptor's range check reads 0 past the key),
+// park them in LDS rows padded by one double (bank spread), and each lane then
+// runs its 16 steps from its row.  Loads run kSpecAhead rounds ahead in
+// registers; LDS is double-buffered, one barrier a round.  Part lengths and
+// warm-ups are whole rounds (multiples of kTdChunk), so every lane's guess
+// falls on a round boundary and only the last part's last round is partial.
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-// the speculative split of long key s (segment [b, e), its state before the
-// batch v0) by the block's kSpecParts threads; returns with the block synced
-__device__ __forceinline__ void td_spec_key(const double* __restrict__ vals, int64_t s, int64_t b, int64_t e,
-                                            double v0, double a, double oma, double* __restrict__ out, int64_t warm,
-                                            double* guess, double* fin, int* missed) {
+constexpr int kSpecParts = 512;   // lanes per block (8 waves): parts of one key, at most
+constexpr int kSpecPart = 512;    // values per part (fewer parts for shorter keys)
+constexpr int kSpecRow = kTdChunk + 1;  // LDS doubles per part row (padded)
+constexpr int kSpecAhead = 3;     // rounds of loads in flight (register sets)
+constexpr int kSpecRowsPerLoad = kSpecParts / kTdChunk;  // rows one load instruction of the block covers
+struct SpecShared {
+    double stage[2][kSpecParts * kSpecRow];
+    double guess[kSpecParts], fin[kSpecParts];
+    int start[kSpecParts];  // a lane's stream start, relative to the key's first value
+    int64_t list[kSpecParts];
+    int miss_any, n_list, rounds;
+};
+// every lane of the block streams [ws, j) of the key's values kv[0, n) from
+// state v (live lanes only; ws and j relative to kv), recording in g its state
+// at i (a round boundary at or after ws)
+__device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, int ws, int i, int j, double& v,
+                                            double& g, double a, double oma, SpecShared& sh) {
     const int p = threadIdx.x;
-    const int64_t n = e - b;
-    const int64_t want = min<int64_t>(kSpecParts, (n + kSpecPart - 1) / kSpecPart);
-    const int64_t len = (n + want - 1) / want;
-    const int parts = (int)((n + len - 1) / len);  // none empty
-    if (p == 0) *missed = 0;
-    if (p < parts) {
-        const int64_t i = b + p * len, j = min(i + len, e);
-        // the warm-up: from the key's state at the segment start (exact), or
-        // from 0 over the `warm` values before the part
-        const int64_t ws = max(b, i - warm);
-        const double g = td_range_deep(ws == b ? v0 : 0.0, vals, ws, i, a, oma);
-        guess[p] = g;
-        fin[p] = td_range_deep(g, vals, i, j, a, oma);
-    }
+    const int rounds_p = live ? (j - ws + kTdChunk - 1) / kTdChunk : 0;
+    const int chk = (i - ws) / kTdChunk;
+    if (p == 0) sh.rounds = 0;
+    sh.start[p] = live ? ws : 0;
     __syncthreads();
-    if (p > 0 && p < parts && __double_as_longlong(guess[p]) != __double_as_longlong(fin[p - 1])) *missed = 1;
+    if (rounds_p) atomicMax(&sh.rounds, rounds_p);
+    // this thread's load slots: row k * kSpecRowsPerLoad + p / 16, column p % 16
+    int off[kTdChunk];
+#pragma unroll
+    for (int k = 0; k < kTdChunk; k++) off[k] = (sh.start[k * kSpecRowsPerLoad + (p >> 4)] + (p & 15)) * 8;
     __syncthreads();
-    if (p == 0) {
-        double v = fin[parts - 1];
-        if (*missed) {  // rare: a warm-up had not converged; rerun from the first miss on
-            v = fin[0];
-            for (int q = 1; q < parts; q++) {
-                const int64_t i = b + q * len, j = min(i + len, e);
-                if (__double_as_longlong(guess[q]) == __double_as_longlong(v)) v = fin[q];
-                else v = td_range_deep(v, vals, i, j, a, oma);
+    const int rounds = __builtin_amdgcn_readfirstlane(sh.rounds);
+    auto fetch = [&](double(&r)[kTdChunk], int round) {
+        const int base = round * kTdChunk;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(kv + base), (short)0, max(n - base, 0) * 8,
+                                                            0x00020000);
+#pragma unroll
+        for (int k = 0; k < kTdChunk; k++)
+            r[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off[k], 0, 0));
+    };
+    auto park = [&](const double(&r)[kTdChunk], int buf) {
+#pragma unroll
+        for (int k = 0; k < kTdChunk; k++)
+            sh.stage[buf][(k * kSpecRowsPerLoad + (p >> 4)) * kSpecRow + (p & 15)] = r[k];
+    };
+    double rg[kSpecAhead][kTdChunk];
+#pragma unroll
+    for (int u = 0; u < kSpecAhead; u++) fetch(rg[u], u);
+    for (int r0 = 0; r0 < rounds; r0 += kSpecAhead) {
+#pragma unroll
+        for (int u = 0; u < kSpecAhead; u++) {
+            const int r = r0 + u;
+            if (r >= rounds) break;  // block-uniform
+            park(rg[u], r & 1);
+            fetch(rg[u], r + kSpecAhead);
+            __syncthreads();  // round r parked; round r - 1's rows (the other buffer) all read
+            if (r < rounds_p) {
+                if (r == chk) g = v;
+                double x[kTdChunk];
+                const double* row = &sh.stage[r & 1][p * kSpecRow];
+#pragma unroll
+                for (int k = 0; k < kTdChunk; k++) x[k] = row[k];
+                const int m = j - ws - r * kTdChunk;
+                v = m >= kTdChunk ? td_run_full(v, x, a, oma) : td_run(v, x, m, a, oma);
             }
         }
-        out[s] = v;
     }
-    __syncthreads();  // guess / fin / missed are free for the next key
+    __syncthreads();  // the stage and start rows are free for the next stream
+}
+// the speculative split of long key s (segment [b, e), its state before the
+// batch v0) by the block's threads; returns with the block synced
+__device__ __forceinline__ void td_spec_key(const double* __restrict__ vals, int64_t s, int64_t b, int64_t e,
+                                            double v0, double a, double oma, double* __restrict__ out, int warm16,
+                                            SpecShared& sh) {
+    const int p = threadIdx.x;
+    if (e - b > (1 << 27)) {  // byte offsets past 2^30: beyond any batch that fits in HBM; sequential
+        if (p == 0) out[s] = td_range(v0, vals, b, e, a, oma);
+        __syncthreads();
+        return;
+    }
+    const int n = (int)(e - b);
+    const double* kv = vals + b;
+    const int want = min(kSpecParts, (n + kSpecPart - 1) / kSpecPart);
+    // whole rounds, an odd number of them: the lanes' rows of one round then
+    // lie an odd multiple of 128 B apart, spread over the HBM channels (at
+    // 1,024 values, 8 KB apart, they fell on few)
+    const int len = ((n + want - 1) / want + kTdChunk - 1) / kTdChunk * kTdChunk | kTdChunk;
+    const int parts = (n + len - 1) / len;  // none empty
+    const bool live = p < parts;
+    // lane p's part [i, j), its warm-up from ws (relative to b; i a round boundary)
+    const int i = p * len, j = min(i + len, n), ws = max(0, i - warm16);
+    double v = ws == 0 ? v0 : 0.0, g = v;
+    spec_stream(kv, n, live, ws, i, j, v, g, a, oma, sh);
+    if (live) {
+        sh.guess[p] = g;
+        sh.fin[p] = v;
+    }
+    // misses: rerun from the predecessor's end until every part matches it
+    for (int pass = 0; pass < kSpecParts; pass++) {
+        if (p == 0) sh.miss_any = 0;
+        __syncthreads();
+        const bool miss = live && p > 0 && __double_as_longlong(sh.guess[p]) != __double_as_longlong(sh.fin[p - 1]);
+        double from = 0.0;
+        if (miss) {
+            from = sh.fin[p - 1];
+            sh.miss_any = 1;
+        }
+        __syncthreads();
+        if (!sh.miss_any) break;  // block-uniform
+        double w = from, unused = from;
+        spec_stream(kv, n, miss, i, i, j, w, unused, a, oma, sh);
+        if (miss) {
+            sh.guess[p] = from;
+            sh.fin[p] = w;
+        }
+    }
+    if (p == 0) out[s] = sh.fin[parts - 1];
+    __syncthreads();  // the shared state is free for the next key
 }
 // Persistent over the long keys: block k of G takes long keys k, k + G,
 // k + 2G, ... (the longest keys are the smallest, the opening's and the
 // first plies', so they land on different blocks), checks kSpecParts of them
 // at once and splits those of >= 4 * warm updates; the rest are
 // td_ema_long_kernel's.  (One block per long key, most of them exiting at
-// once, cost a block slot each at this kernel's one block per CU.)
+// once, cost a block slot each.)
 __global__ __launch_bounds__(kSpecParts) void td_ema_spec_kernel(const double* __restrict__ vals,
                                                                  const int64_t* __restrict__ seg_off,
                                                                  const double* __restrict__ init, double a, double oma,
                                                                  double* __restrict__ out,
                                                                  const int64_t* __restrict__ long_idx, int64_t n_long,
                                                                  int64_t warm) {
-    __shared__ double guess[kSpecParts], fin[kSpecParts];
-    __shared__ int missed, n_list;
-    __shared__ int64_t list[kSpecParts];
+    __shared__ SpecShared sh;
     if (warm <= 0) return;
+    const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
     const int64_t G = gridDim.x;
     for (int64_t k0 = blockIdx.x; k0 < n_long; k0 += G * kSpecParts) {
-        if (threadIdx.x == 0) n_list = 0;
+        if (threadIdx.x == 0) sh.n_list = 0;
         __syncthreads();
         const int64_t k = k0 + (int64_t)threadIdx.x * G;
         if (k < n_long) {
             const int64_t s = long_idx[k];
-            if (seg_off[s + 1] - seg_off[s] >= 4 * warm) list[atomicAdd(&n_list, 1)] = s;
+            if (seg_off[s + 1] - seg_off[s] >= 4 * warm) sh.list[atomicAdd(&sh.n_list, 1)] = s;
         }
         __syncthreads();
-        const int m = n_list;
+        const int m = sh.n_list;
         for (int q = 0; q < m; q++) {
-            const int64_t s = list[q];
-            td_spec_key(vals, s, seg_off[s], seg_off[s + 1], init ? init[s] : 0.0, a, oma, out, warm, guess, fin,
-                        &missed);
+            // wave-uniform by construction; said so, the key's descriptor is built in SGPRs
+            const int64_t s = uniform64(sh.list[q]);
+            td_spec_key(vals, s, seg_off[s], seg_off[s + 1], init ? init[s] : 0.0, a, oma, out, warm16, sh);
         }
     }
 }

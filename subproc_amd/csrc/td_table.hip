@@ -26,9 +26,21 @@
 
 namespace {
 
+// onesweep digit width and items per thread (build knobs for A/B builds only:
+// tools/gpu_ab.sh; the product build uses the defaults)
+#ifndef OTH_SORT_BITS
+#define OTH_SORT_BITS 9
+#endif
+#ifndef OTH_SORT_IPT
+#define OTH_SORT_IPT 8
+#endif
+#ifndef OTH_SORT_BLOCK
+#define OTH_SORT_BLOCK 1024
+#endif
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 9,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<OTH_SORT_BLOCK, OTH_SORT_IPT>,
+                                        rocprim::kernel_config<OTH_SORT_BLOCK, OTH_SORT_IPT>, OTH_SORT_BITS,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
 // packed words -> (key, value): the value recomputed from the payload exactly

@@ -65,9 +65,9 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
     sequential rule in Python floats.  With long_min, oth_td_ema_split runs
     the segments at least that long on a whole wave each (LDS stages of 1024
     values: lengths around multiples of the stage), those at least 4 warm-ups
-    long split into parts over the wave's lanes (warm-up 64 at a = 0.5).  A
+    long split into parts over a block's lanes (warm-up 64 at a = 0.5).  A
     warm-up of 1 or 3 values (OTH_TD_SPEC_WARM) makes most guesses miss: the
-    rerun path."""
+    rerun passes."""
     from subproc_amd import _lib
     if spec_warm is not None:
         monkeypatch.setenv("OTH_TD_SPEC_WARM", spec_warm)
@@ -106,7 +106,8 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
 @pytest.mark.parametrize("kind", ["normal", "constant", "sparse"])
 def test_td_ema_split_speculation_learner_rate(kind):
     """Long segments at the learner's rate (a = 0.03, warm-up 1457 values) split
-    over up to 64 lanes: the result is the sequential rule's, bit for bit,
+    over up to 512 lanes (600,001 values: 512 parts of 1,184): the result is the
+    sequential rule's, bit for bit,
     whether the lanes' guesses converge (random targets), sit on a fixed
     point of the rounding (a constant target) or run through exact zeros
     (mostly-zero targets: draws)."""
@@ -114,7 +115,7 @@ def test_td_ema_split_speculation_learner_rate(kind):
     a = 0.03
     oma = 1 - a
     rng = np.random.default_rng({"normal": 5, "constant": 6, "sparse": 7}[kind])
-    lengths = [5827, 5828, 9000, 70001, 200003]
+    lengths = [5827, 5828, 9000, 70001, 200003, 600001]
     vals, seg, want = [], [0], []
     for L in lengths:
         if kind == "normal":

@@ -13,8 +13,13 @@ import torch  # noqa: E402
 from subproc_amd import ops  # noqa: E402
 from subproc_amd.td import StateMap  # noqa: E402
 
-games = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
-reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+args = [x for x in sys.argv[1:] if not x.startswith("--lib=")]
+for x in sys.argv[1:]:
+    if x.startswith("--lib="):  # an A/B build of the whole library (tools/gpu_ab.sh)
+        from subproc_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(x[len("--lib="):])
+games = int(args[0]) if len(args) > 0 else 1 << 18
+reps = int(args[1]) if len(args) > 1 else 3
 dev = torch.device("cuda", 0)
 sm = StateMap(dev)
 for k in range(reps):

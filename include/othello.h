@@ -301,14 +301,20 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
 /* oth_td_ema with the long segments split off: segments of length >= long_min
  * are each run by a whole wavefront, the others one per thread as in
  * oth_td_ema.  Such a wave runs a segment on one lane from LDS stages or, if
- * the rule contracts (|1 - a| < 1) and the segment is long enough, as up to
- * 64 parts on its lanes from warm-up guesses of each part's start state, each
- * guess verified bit for bit and a part rerun when its guess missed.  long_idx (device, n_long entries) must list every segment of
+ * the rule contracts (|1 - a| < 1) and the segment is long enough, as parts
+ * of ~1,000 updates on many waves from warm-up guesses of each part's start
+ * state, each guess verified bit for bit and a part rerun when its guess
+ * missed.  long_idx (device, n_long entries) must list every segment of
  * length >= long_min, in any order, each once; a segment that long missing
- * from it is left unwritten.  Same results as oth_td_ema, bit for bit. */
+ * from it is left unwritten.  n_values = seg_off[n_seg], the length of
+ * values.  temp / temp_bytes: device scratch of the split (its plan, the
+ * parts' guesses and end states), the caller's; temp == NULL is a size query
+ * (*temp_bytes receives the size for these n_long and n_values, nothing else
+ * happens), otherwise *temp_bytes is the size of temp.  Same results as
+ * oth_td_ema, bit for bit. */
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
-                     int64_t n_long, void* stream);
+                     int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream);
 
 /* Packed updates (the GPU books' path, StateMap.update): the update stream
  * of oth_td_updates / oth_td_updates_rows (row_off NULL: the strided table)

@@ -338,9 +338,14 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
 
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
-                     int64_t n_long, void* stream) {
-    /* the split only changes how the GPU schedules segments: every segment in order here */
-    if (long_min < 1 || n_long < 0 || (n_long > 0 && !long_idx)) return OTH_EINVAL;
+                     int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream) {
+    /* the split only changes how the GPU schedules segments: every segment in
+       order here, no scratch */
+    if (long_min < 1 || n_long < 0 || n_values < 0 || !temp_bytes || (n_long > 0 && !long_idx)) return OTH_EINVAL;
+    if (!temp) {
+        *temp_bytes = 0;
+        return OTH_OK;
+    }
     return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
 }
 

@@ -1553,70 +1553,81 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
 
 // Speculative split of a very long segment (the opening position's key gets
 // one update per game and side; the first plies' keys a fraction of that)
-// over up to kSpecParts lanes of one block.  The rule is a contraction
-// (|1 - a| < 1): two runs over the same values from different states approach
-// each other by |1 - a| per step and, once a rounding maps them to the same
-// double, mostly stay equal.  So the lane of part p > 0 guesses the state at
-// the start of its part by a warm-up run over the `warm` values before it,
-// from state 0 (the rule then starts at the first value itself), or exactly,
-// from the key's initial state, when the part starts within `warm` of the
-// segment; `warm` is sized by the launcher so that |1 - a|^warm < 2^-64.
-// Lane p then runs its part from the guess.  A part whose guess equals the
-// end state of the part before, itself exact, ran from the exact state; part
-// 0 is exact.  The guesses that missed (the last ulp had not merged yet: ~1 in
-// 1,000 parts, tools/diag/td_spec_probe.py) are rerun by their lanes in
-// parallel from the end state of the part before, and the check repeats until
+// into parts of kSpecLen updates, run side by side.  The rule is a
+// contraction (|1 - a| < 1): two runs over the same values from different
+// states approach each other by |1 - a| per step and, once a rounding maps
+// them to the same double, mostly stay equal.  So the lane of part p > 0
+// guesses the state at the start of its part by a warm-up run over the
+// `warm` values before it, from state 0 (the rule then starts at the first
+// value itself), or exactly, from the key's initial state, when the part
+// starts within `warm` of the segment; `warm` is sized by the launcher so
+// that |1 - a|^warm < 2^-64.  Lane p then runs its part from the guess.  A
+// part whose guess equals the end state of the part before, itself exact, ran
+// from the exact state; part 0 is exact.  The guesses that missed (the last
+// ulp had not merged yet: ~1 in 1,000 parts, tools/diag/td_spec_probe.py) are
+// rerun from the end state of the part before, and the check repeats until
 // every part matches its predecessor; each pass fixes at least the first
 // miss.  Every result is thus the sequential one; speculation only decides
 // how fast it comes.
-// Feeding the lanes: each lane streams its own range, so a lane-private load
-// touches 64 cache lines per wave instruction (round 4's first version: 1,024
-// line lookups per wave per 16 steps, 486-676 us per launch at ~190 ns a
-// step).  Here the block moves its parts' values in rounds of kTdChunk per
-// lane: the threads load the round's parts x 16 doubles cooperatively (a wave
-// instruction covers 4 rows of 16 consecutive doubles: 4-8 lines) through a
-// buffer descriptor that advances 16 doubles a round (fixed per-lane offsets,
-// no address arithmetic; the descriptor's range check reads 0 past the key),
-// park them in LDS rows padded by one double (bank spread), and each lane then
-// runs its 16 steps from its row.  Loads run kSpecAhead rounds ahead in
-// registers; LDS is double-buffered, one barrier a round.  Part lengths and
-// warm-ups are whole rounds (multiples of kTdChunk), so every lane's guess
-// falls on a round boundary and only the last part's last round is partial.
+//
+// Three launches: td_spec_plan_kernel lists the keys to split with their
+// parts and work items (a wave's 64 consecutive parts); td_spec_parts_kernel
+// runs every work item as a one-wave block, so one key's parts spread over
+// as many CUs as it has work items; td_spec_fix_kernel checks each key's
+// parts in order and reruns the misses.  (Round 4's first versions ran a
+// key's parts in one block of 256 or 512 lanes: 0.8-2 us a round of 16 steps,
+// growing with the lanes of the block -- one CU's load path -- 320-430 us per
+// launch for the opening key.)
+// Feeding a wave: each lane streams its own range, so lane-private loads would
+// touch 64 cache lines per wave instruction.  Instead the wave moves its
+// parts' values in rounds of kTdChunk per lane: it loads the round's 64 x 16
+// doubles cooperatively (one load instruction covers 4 rows of 16 consecutive
+// doubles) through a buffer descriptor that advances 16 doubles a round
+// (fixed per-lane offsets, no address arithmetic; the descriptor's range check
+// reads 0 past the key), parks them in LDS rows padded by one double (bank
+// spread), and each lane then runs its 16 steps from its row.  Loads run
+// kSpecAhead rounds ahead in registers; LDS is double-buffered.  Part lengths
+// and warm-ups are whole rounds, so every lane's guess falls on a round
+// boundary and only a key's last part ends inside a round.
+constexpr int kSpecLanes = 64;          // parts per work item (one wave)
+constexpr int kSpecLen = 1040;          // updates per part: 65 rounds, an odd number (rows
+                                        // of one round an odd multiple of 128 B apart)
+constexpr int kSpecRow = kTdChunk + 1;  // LDS doubles per part row (padded)
+constexpr int kSpecAhead = 3;           // rounds of loads in flight (register sets)
+constexpr int kSpecRowsPerLoad = kSpecLanes / kTdChunk;
+struct SpecWave {
+    double stage[2][kSpecLanes * kSpecRow];
+    int start[kSpecLanes];  // a lane's stream start, relative to the key's first value
+    int rounds;
+};
+struct SpecPlanEntry {
+    int64_t s, part_base, item_base, n_parts;
+};
+constexpr int kSpecHdr = 8;  // int64 header of the scratch: [0] keys split, [1] work items, [2] parts
+constexpr int64_t kSpecMaxLen = 1ll << 27;  // longer keys (beyond any batch in HBM) stay sequential
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-constexpr int kSpecParts = 512;   // lanes per block (8 waves): parts of one key, at most
-constexpr int kSpecPart = 512;    // values per part (fewer parts for shorter keys)
-constexpr int kSpecRow = kTdChunk + 1;  // LDS doubles per part row (padded)
-constexpr int kSpecAhead = 3;     // rounds of loads in flight (register sets)
-constexpr int kSpecRowsPerLoad = kSpecParts / kTdChunk;  // rows one load instruction of the block covers
-struct SpecShared {
-    double stage[2][kSpecParts * kSpecRow];
-    double guess[kSpecParts], fin[kSpecParts];
-    int start[kSpecParts];  // a lane's stream start, relative to the key's first value
-    int64_t list[kSpecParts];
-    int miss_any, n_list, rounds;
-};
-// every lane of the block streams [ws, j) of the key's values kv[0, n) from
-// state v (live lanes only; ws and j relative to kv), recording in g its state
-// at i (a round boundary at or after ws)
+// the wave streams [ws, j) of the key's values kv[0, n) from state v (live
+// lanes only; ws and j relative to kv), recording in g its state at i (a
+// round boundary at or after ws).  kv and n wave-uniform.
 __device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, int ws, int i, int j, double& v,
-                                            double& g, double a, double oma, SpecShared& sh) {
+                                            double& g, double a, double oma, SpecWave& sh) {
     const int p = threadIdx.x;
     const int rounds_p = live ? (j - ws + kTdChunk - 1) / kTdChunk : 0;
     const int chk = (i - ws) / kTdChunk;
-    if (p == 0) sh.rounds = 0;
     sh.start[p] = live ? ws : 0;
-    __syncthreads();
-    if (rounds_p) atomicMax(&sh.rounds, rounds_p);
-    // this thread's load slots: row k * kSpecRowsPerLoad + p / 16, column p % 16
+    int rmax = rounds_p;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rmax = max(rmax, __shfl_xor(rmax, o));
+    const int rounds = __builtin_amdgcn_readfirstlane(rmax);
+    wave_sync();
+    // this lane's load slots: row k * kSpecRowsPerLoad + p / 16, column p % 16
     int off[kTdChunk];
 #pragma unroll
     for (int k = 0; k < kTdChunk; k++) off[k] = (sh.start[k * kSpecRowsPerLoad + (p >> 4)] + (p & 15)) * 8;
-    __syncthreads();
-    const int rounds = __builtin_amdgcn_readfirstlane(sh.rounds);
     auto fetch = [&](double(&r)[kTdChunk], int round) {
         const int base = round * kTdChunk;
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(kv + base), (short)0, max(n - base, 0) * 8,
@@ -1637,10 +1648,10 @@ __device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, 
 #pragma unroll
         for (int u = 0; u < kSpecAhead; u++) {
             const int r = r0 + u;
-            if (r >= rounds) break;  // block-uniform
+            if (r >= rounds) break;  // wave-uniform
             park(rg[u], r & 1);
             fetch(rg[u], r + kSpecAhead);
-            __syncthreads();  // round r parked; round r - 1's rows (the other buffer) all read
+            wave_sync();  // round r parked (a wave's LDS ops are in order)
             if (r < rounds_p) {
                 if (r == chk) g = v;
                 double x[kTdChunk];
@@ -1652,90 +1663,154 @@ __device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, 
             }
         }
     }
-    __syncthreads();  // the stage and start rows are free for the next stream
+    wave_sync();  // the stage and start rows are free for the next stream
 }
-// the speculative split of long key s (segment [b, e), its state before the
-// batch v0) by the block's threads; returns with the block synced
-__device__ __forceinline__ void td_spec_key(const double* __restrict__ vals, int64_t s, int64_t b, int64_t e,
-                                            double v0, double a, double oma, double* __restrict__ out, int warm16,
-                                            SpecShared& sh) {
-    const int p = threadIdx.x;
-    if (e - b > (1 << 27)) {  // byte offsets past 2^30: beyond any batch that fits in HBM; sequential
-        if (p == 0) out[s] = td_range(v0, vals, b, e, a, oma);
-        __syncthreads();
-        return;
-    }
-    const int n = (int)(e - b);
-    const double* kv = vals + b;
-    const int want = min(kSpecParts, (n + kSpecPart - 1) / kSpecPart);
-    // whole rounds, an odd number of them: the lanes' rows of one round then
-    // lie an odd multiple of 128 B apart, spread over the HBM channels (at
-    // 1,024 values, 8 KB apart, they fell on few)
-    const int len = ((n + want - 1) / want + kTdChunk - 1) / kTdChunk * kTdChunk | kTdChunk;
-    const int parts = (n + len - 1) / len;  // none empty
-    const bool live = p < parts;
-    // lane p's part [i, j), its warm-up from ws (relative to b; i a round boundary)
-    const int i = p * len, j = min(i + len, n), ws = max(0, i - warm16);
-    double v = ws == 0 ? v0 : 0.0, g = v;
-    spec_stream(kv, n, live, ws, i, j, v, g, a, oma, sh);
-    if (live) {
-        sh.guess[p] = g;
-        sh.fin[p] = v;
-    }
-    // misses: rerun from the predecessor's end until every part matches it
-    for (int pass = 0; pass < kSpecParts; pass++) {
-        if (p == 0) sh.miss_any = 0;
-        __syncthreads();
-        const bool miss = live && p > 0 && __double_as_longlong(sh.guess[p]) != __double_as_longlong(sh.fin[p - 1]);
-        double from = 0.0;
-        if (miss) {
-            from = sh.fin[p - 1];
-            sh.miss_any = 1;
+// the parts of a key of n updates
+__device__ __forceinline__ int64_t spec_parts(int64_t n) { return (n + kSpecLen - 1) / kSpecLen; }
+
+// one block: the keys of >= spec_min updates among the long keys, in
+// long_idx order, with their parts' and work items' running offsets
+__global__ __launch_bounds__(1024) void td_spec_plan_kernel(const int64_t* __restrict__ seg_off,
+                                                            const int64_t* __restrict__ long_idx, int64_t n_long,
+                                                            int64_t spec_min, int64_t* __restrict__ hdr,
+                                                            SpecPlanEntry* __restrict__ plan) {
+    __shared__ u32 wsum[3][16];
+    __shared__ int64_t carry[3];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t < 3) carry[t] = 0;
+    __syncthreads();
+    // kPlanBatch tiles of 1,024 keys at a time: their loads all issued before
+    // the first is used (two dependent round trips per batch, not per tile)
+    constexpr int kPlanBatch = 8;
+    for (int64_t b0 = 0; b0 < n_long; b0 += 1024 * kPlanBatch) {
+      int64_t sb[kPlanBatch], lo[kPlanBatch], hi[kPlanBatch];
+#pragma unroll
+      for (int u = 0; u < kPlanBatch; u++) {
+          const int64_t k = b0 + u * 1024 + t;
+          sb[u] = k < n_long ? long_idx[k] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kPlanBatch; u++) {
+          lo[u] = sb[u] >= 0 ? seg_off[sb[u]] : 0;
+          hi[u] = sb[u] >= 0 ? seg_off[sb[u] + 1] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kPlanBatch; u++) {
+        const int64_t t0 = b0 + u * 1024;
+        if (t0 >= n_long) break;  // block-uniform
+        const int64_t s = sb[u], n = hi[u] - lo[u];
+        const bool f = s >= 0 && n >= spec_min && n <= kSpecMaxLen;
+        const u32 P = f ? (u32)spec_parts(n) : 0u, C = (P + kSpecLanes - 1) / kSpecLanes;
+        // block-wide exclusive scans of (f, P, C): lanes by DPP, waves through LDS
+        const u32 in[3] = {f ? 1u : 0u, P, C};
+        u32 incl[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            incl[c] = wave_incl_scan(in[c]);
+            if (lane == 63) wsum[c][wv] = incl[c];
         }
         __syncthreads();
-        if (!sh.miss_any) break;  // block-uniform
-        double w = from, unused = from;
-        spec_stream(kv, n, miss, i, i, j, w, unused, a, oma, sh);
-        if (miss) {
-            sh.guess[p] = from;
-            sh.fin[p] = w;
+        int64_t ex[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            u32 before = 0;
+            for (int w2 = 0; w2 < wv; w2++) before += wsum[c][w2];
+            ex[c] = carry[c] + before + incl[c] - in[c];
         }
+        if (f) plan[ex[0]] = SpecPlanEntry{s, ex[1], ex[2], (int64_t)P};
+        __syncthreads();
+        if (t < 3) {
+            u32 tot = 0;
+            for (int w2 = 0; w2 < 16; w2++) tot += wsum[t][w2];
+            carry[t] += tot;
+        }
+        __syncthreads();
+      }
     }
-    if (p == 0) out[s] = sh.fin[parts - 1];
-    __syncthreads();  // the shared state is free for the next key
+    if (t < 3) hdr[t] = carry[t];
 }
-// Persistent over the long keys: block k of G takes long keys k, k + G,
-// k + 2G, ... (the longest keys are the smallest, the opening's and the
-// first plies', so they land on different blocks), checks kSpecParts of them
-// at once and splits those of >= 4 * warm updates; the rest are
-// td_ema_long_kernel's.  (One block per long key, most of them exiting at
-// once, cost a block slot each.)
-__global__ __launch_bounds__(kSpecParts) void td_ema_spec_kernel(const double* __restrict__ vals,
-                                                                 const int64_t* __restrict__ seg_off,
-                                                                 const double* __restrict__ init, double a, double oma,
-                                                                 double* __restrict__ out,
-                                                                 const int64_t* __restrict__ long_idx, int64_t n_long,
-                                                                 int64_t warm) {
-    __shared__ SpecShared sh;
-    if (warm <= 0) return;
-    const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
-    const int64_t G = gridDim.x;
-    for (int64_t k0 = blockIdx.x; k0 < n_long; k0 += G * kSpecParts) {
-        if (threadIdx.x == 0) sh.n_list = 0;
-        __syncthreads();
-        const int64_t k = k0 + (int64_t)threadIdx.x * G;
-        if (k < n_long) {
-            const int64_t s = long_idx[k];
-            if (seg_off[s + 1] - seg_off[s] >= 4 * warm) sh.list[atomicAdd(&sh.n_list, 1)] = s;
-        }
-        __syncthreads();
-        const int m = sh.n_list;
-        for (int q = 0; q < m; q++) {
-            // wave-uniform by construction; said so, the key's descriptor is built in SGPRs
-            const int64_t s = uniform64(sh.list[q]);
-            td_spec_key(vals, s, seg_off[s], seg_off[s + 1], init ? init[s] : 0.0, a, oma, out, warm16, sh);
+// the key of work item w: the last plan entry whose first item is <= w
+__device__ __forceinline__ int64_t spec_key_of(const SpecPlanEntry* plan, int64_t n_spec, int64_t w) {
+    int64_t lo = 0, hi = n_spec - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (plan[mid].item_base <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// one wave per work item: parts q = 64 c + lane of its key, guesses and end states out
+__global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double* __restrict__ vals,
+                                                                   const int64_t* __restrict__ seg_off,
+                                                                   const double* __restrict__ init, double a,
+                                                                   double oma, const int64_t* __restrict__ hdr,
+                                                                   const SpecPlanEntry* __restrict__ plan,
+                                                                   double* __restrict__ guess,
+                                                                   double* __restrict__ fin, int warm16) {
+    __shared__ SpecWave sh;
+    const int64_t n_spec = uniform64(hdr[0]), items = uniform64(hdr[1]);
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const int64_t key = uniform64(spec_key_of(plan, n_spec, w));
+        const int64_t s = uniform64(plan[key].s), pb = uniform64(plan[key].part_base);
+        const int64_t ib = uniform64(plan[key].item_base), np = uniform64(plan[key].n_parts);
+        const int64_t b = uniform64(seg_off[s]);
+        const int n = (int)uniform64(seg_off[s + 1] - b);
+        const int64_t q = (w - ib) * kSpecLanes + threadIdx.x;
+        const bool live = q < np;
+        const int i = (int)q * kSpecLen, j = live ? min(i + kSpecLen, n) : i, ws = max(0, i - warm16);
+        double v = (ws == 0 && init) ? init[s] : 0.0, g = v;
+        spec_stream(vals + b, n, live, ws, i, j, v, g, a, oma, sh);
+        if (live) {
+            guess[pb + q] = g;
+            fin[pb + q] = v;
         }
     }
+}
+// one wave per split key: its parts checked in order, 64 at a time; missed
+// guesses rerun from their predecessor's end state until all match
+__global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* __restrict__ vals,
+                                                                 const int64_t* __restrict__ seg_off, double a,
+                                                                 double oma, const int64_t* __restrict__ hdr,
+                                                                 const SpecPlanEntry* __restrict__ plan,
+                                                                 const double* __restrict__ guess,
+                                                                 const double* __restrict__ fin,
+                                                                 double* __restrict__ out) {
+    __shared__ SpecWave sh;
+    const int lane = threadIdx.x;
+    const int64_t n_spec = uniform64(hdr[0]);
+    for (int64_t key = blockIdx.x; key < n_spec; key += gridDim.x) {
+        const int64_t s = uniform64(plan[key].s), pb = uniform64(plan[key].part_base);
+        const int64_t np = uniform64(plan[key].n_parts);
+        const int64_t b = uniform64(seg_off[s]);
+        const int n = (int)uniform64(seg_off[s + 1] - b);
+        double prev = 0.0;  // the end state of the part before this chunk's first
+        for (int64_t c0 = 0; c0 < np; c0 += kSpecLanes) {
+            const int64_t q = c0 + lane;
+            const bool live = q < np;
+            double g = live ? guess[pb + q] : 0.0, f = live ? fin[pb + q] : 0.0;
+            for (int pass = 0; pass <= kSpecLanes; pass++) {  // each pass fixes the first miss at least
+                double pred = __shfl_up(f, 1);
+                if (lane == 0) pred = prev;
+                const bool miss = live && q > 0 && __double_as_longlong(g) != __double_as_longlong(pred);
+                if (!__ballot(miss)) break;  // wave-uniform
+                const int i = (int)q * kSpecLen, j = miss ? min(i + kSpecLen, n) : i;
+                double w = pred, unused = pred;
+                spec_stream(vals + b, n, miss, i, i, j, w, unused, a, oma, sh);
+                if (miss) {
+                    g = pred;
+                    f = w;
+                }
+            }
+            prev = __shfl(f, (int)min<int64_t>(kSpecLanes - 1, np - 1 - c0));
+        }
+        if (lane == 0) out[s] = prev;
+    }
+}
+// the scratch of the split: header, plan entries, guesses and end states
+inline size_t spec_scratch_bytes(int64_t n_long, int64_t n_values) {
+    const int64_t parts = n_values / kSpecLen + n_long + 1;  // sum of ceil(n / kSpecLen) over <= n_long keys
+    return sizeof(int64_t) * kSpecHdr + sizeof(SpecPlanEntry) * (size_t)std::max<int64_t>(n_long, 1) +
+           2 * sizeof(double) * (size_t)parts;
 }
 
 // One long segment per single-wave block.  A thread alone is bound by how many
@@ -1756,7 +1831,7 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
     const int lane = threadIdx.x;
     const int64_t s = long_idx[blockIdx.x];
     const int64_t b = seg_off[s], e = seg_off[s + 1];
-    if (warm > 0 && e - b >= 4 * warm) return;  // td_ema_spec_kernel's segment
+    if (warm > 0 && e - b >= 4 * warm && e - b <= kSpecMaxLen) return;  // a split key (td_spec_*)
     const int64_t n_stage = (e - b + kTdStage - 1) / kTdStage;
     double r[kTdStageLoads];
     auto fetch = [&](int64_t c) {
@@ -2192,10 +2267,17 @@ static int64_t td_spec_warm(double oma) {
 
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
-                     int64_t n_long, void* stream) {
-    if (n_seg < 0 || long_min < 1 || n_long < 0 || n_long > n_seg ||
+                     int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream) {
+    if (n_seg < 0 || long_min < 1 || n_long < 0 || n_long > n_seg || n_values < 0 || !temp_bytes ||
         (n_seg > 0 && (!values || !seg_off || !out)) || (n_long > 0 && !long_idx))
         return OTH_EINVAL;
+    const int64_t warm = td_spec_warm(one_minus_a);
+    const size_t need = warm > 0 && n_long > 0 ? spec_scratch_bytes(n_long, n_values) : 0;
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (*temp_bytes < need) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
     if (long_min <= 3 * kTdChunk)
         td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
@@ -2205,13 +2287,28 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
                                                                                     one_minus_a, out, n_seg, long_min);
     int rc = launched();
     if (rc != OTH_OK || n_long == 0) return rc;
-    const int64_t warm = td_spec_warm(one_minus_a);
     td_ema_long_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
                                                                          out, long_idx, warm);
     rc = launched();
     if (rc != OTH_OK || warm <= 0) return rc;
-    td_ema_spec_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecParts, 0, (hipStream_t)stream>>>(
-        values, seg_off, init, a, one_minus_a, out, long_idx, n_long, warm);
+    // the split keys: plan, parts (one wave per 64 parts), check and reruns
+    int64_t* hdr = static_cast<int64_t*>(temp);
+    SpecPlanEntry* plan = reinterpret_cast<SpecPlanEntry*>(hdr + kSpecHdr);
+    double* guess = reinterpret_cast<double*>(plan + std::max<int64_t>(n_long, 1));
+    const int64_t parts = n_values / kSpecLen + n_long + 1;
+    double* fin = guess + parts;
+    const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
+    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long, 4 * warm, hdr, plan);
+    rc = launched();
+    if (rc != OTH_OK) return rc;
+    const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
+    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                   one_minus_a, hdr, plan, guess,
+                                                                                   fin, warm16);
+    rc = launched();
+    if (rc != OTH_OK) return rc;
+    td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, (hipStream_t)stream>>>(
+        values, seg_off, a, one_minus_a, hdr, plan, guess, fin, out);
     return launched();
 }
 

@@ -242,9 +242,10 @@ class StateMap:
             # keys with many updates (the opening and the first plies of every
             # game) are each run by a whole wavefront (oth_td_ema_split)
             long_idx = torch.nonzero(counts >= LONG_MIN).flatten()
-            check(lib.oth_td_ema_split(sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a, 1 - self.a,
-                                       out.data_ptr(), ukeys.numel(), LONG_MIN, long_idx.data_ptr(),
-                                       long_idx.numel(), stream), "oth_td_ema_split")
+            _with_scratch(lib.oth_td_ema_split, (sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a,
+                                                 1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN,
+                                                 long_idx.data_ptr(), long_idx.numel(), sv.numel()),
+                          stream, self.device, "oth_td_ema_split")
             if is_new is None:
                 self.keys, self.values = ukeys, out
             else:

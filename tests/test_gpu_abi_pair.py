@@ -381,7 +381,7 @@ def test_td_pair():
     li = Buf(np.flatnonzero(lens >= 48).astype(np.int64))
     assert 0 < len(li.h) < len(uk)
     out2 = Buf(np.zeros(len(uk), np.float64))
-    both("oth_td_ema_split", sv, seg, init, 0.03, 1 - 0.03, out2, len(uk), 48, li, len(li.h))
+    both_scratch("oth_td_ema_split", sv, seg, init, 0.03, 1 - 0.03, out2, len(uk), 48, li, len(li.h), total)
     same(out2)
     np.testing.assert_array_equal(out2.h, out.h)
 
@@ -415,7 +415,11 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_eval(None, None, w, None, 0, s) == 0
         assert lib.oth_td_updates(None, None, None, None, None, None, 0, s) == 0
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 0, s) == 0
-        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 1, None, 0, s) == 0
+        tb0 = ctypes.c_size_t(0)
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 1, None, 0, 0, None, ctypes.byref(tb0),
+                                    s) == 0  # size query
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 1, None, 0, 0, ctypes.c_void_p(8),
+                                    ctypes.byref(tb0), s) == 0
         assert lib.oth_sample_midgame(1, 0, None, None, None, None, 0, s) == 0
         E = _lib.OTH_EINVAL
         assert lib.oth_step(None, None, None, None, None, None, None, None, None, 5, s) == E
@@ -428,7 +432,10 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_hands(None, None, None, None, None, None, None, 3, s) == E
         assert lib.oth_eval(None, None, None, None, 0, s) == E
         assert lib.oth_td_ema(None, None, None, 0.03, 0.97, None, 3, s) == E
-        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 0, None, 0, s) == E  # long_min < 1
+        tb0 = ctypes.c_size_t(0)
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 0, None, 0, 0, None, ctypes.byref(tb0),
+                                    s) == E  # long_min < 1
+        assert lib.oth_td_ema_split(None, None, None, 0.03, 0.97, None, 0, 1, None, 0, 0, None, None, s) == E  # no size
         tb = ctypes.c_size_t(0)
         assert lib.oth_td_sort_pairs(None, None, None, None, 0, None, ctypes.byref(tb), s) == 0  # size query
         assert lib.oth_td_sort_pairs(None, None, None, None, 0, ctypes.c_void_p(8), ctypes.byref(tb), s) == 0

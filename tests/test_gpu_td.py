@@ -98,8 +98,9 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
                                   len(lengths), st), "oth_td_ema")
     else:
         li = torch.tensor([i for i, L in enumerate(lengths) if L >= long_min][::-1], dtype=torch.int64, device=DEV)
-        _lib.check(lib.oth_td_ema_split(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
-                                        len(lengths), long_min, li.data_ptr(), li.numel(), st), "oth_td_ema_split")
+        td._with_scratch(lib.oth_td_ema_split, (dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma,
+                                                out.data_ptr(), len(lengths), long_min, li.data_ptr(), li.numel(),
+                                                dv.numel()), st, DEV, "oth_td_ema_split")
     assert out.cpu().tolist() == [w[1] for w in want]
 
 
@@ -136,9 +137,9 @@ def test_td_ema_split_speculation_learner_rate(kind):
     out = torch.empty(len(lengths), dtype=torch.float64, device=DEV)
     li = torch.arange(len(lengths), dtype=torch.int64, device=DEV)
     lib = _lib.load()
-    _lib.check(lib.oth_td_ema_split(dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
-                                    len(lengths), 1024, li.data_ptr(), li.numel(),
-                                    torch.cuda.current_stream().cuda_stream), "oth_td_ema_split")
+    td._with_scratch(lib.oth_td_ema_split, (dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
+                                            len(lengths), 1024, li.data_ptr(), li.numel(), dv.numel()),
+                     torch.cuda.current_stream().cuda_stream, DEV, "oth_td_ema_split")
     assert out.cpu().tolist() == want
 
 

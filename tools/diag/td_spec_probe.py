@@ -16,7 +16,12 @@ import torch  # noqa: E402
 from subproc_amd import ops, td  # noqa: E402
 from subproc_amd._lib import load  # noqa: E402
 
-games = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+args = [x for x in sys.argv[1:] if not x.startswith("--lib=")]
+for x in sys.argv[1:]:
+    if x.startswith("--lib="):  # an A/B build of the whole library
+        from subproc_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(x[len("--lib="):])
+games = int(args[0]) if args else 1 << 18
 dev = torch.device("cuda", 0)
 sm = td.StateMap(dev)
 cap = {}
@@ -35,7 +40,7 @@ for k in range(2):
     sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
 torch.cuda.synchronize()
 a, oma = sm.a, 1 - sm.a
-warm = math.ceil(-64 * math.log(2) / math.log(abs(oma)))
+warm = int(os.environ.get("OTH_TD_SPEC_WARM", 0)) or math.ceil(-64 * math.log(2) / math.log(abs(oma)))
 warm16 = (warm + 15) // 16 * 16
 sk, sv = cap["sk"], cap["sv"]
 ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
@@ -62,8 +67,7 @@ inith = init.cpu().numpy()
 for s in spec[:40]:
     b, e = int(segh[s]), int(segh[s + 1])
     n = e - b
-    want = min(512, (n + 511) // 512)
-    ln = ((n + want - 1) // want + 15) // 16 * 16 | 16
+    ln = 1040  # kSpecLen
     parts = (n + ln - 1) // ln
     x = svh[b:e].tolist()
     v = float(inith[s])
@@ -86,8 +90,10 @@ st = torch.cuda.current_stream()
 for rep in range(3):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    rc = lib.oth_td_ema_split(sv.data_ptr(), seg.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(), ukeys.numel(),
-                              td.LONG_MIN, long_idx.data_ptr(), long_idx.numel(), st.cuda_stream)
+    td._with_scratch(lib.oth_td_ema_split, (sv.data_ptr(), seg.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
+                                            ukeys.numel(), td.LONG_MIN, long_idx.data_ptr(), long_idx.numel(),
+                                            sv.numel()), st.cuda_stream, dev, "oth_td_ema_split")
+    rc = 0
     e1.record(st)
     torch.cuda.synchronize()
     print("oth_td_ema_split rc %d: %.1f us" % (rc, e0.elapsed_time(e1) * 1e3), flush=True)

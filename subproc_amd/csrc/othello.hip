@@ -1603,7 +1603,7 @@ struct SpecWave {
 struct SpecPlanEntry {
     int64_t s, part_base, item_base, n_parts;
 };
-constexpr int kSpecHdr = 8;  // int64 header of the scratch: [0] keys split, [1] work items, [2] parts
+constexpr int kSpecHdr = 8;  // int64 header of the scratch: [0] keys split, [1] work items, [2] parts, [3] counter
 constexpr int64_t kSpecMaxLen = 1ll << 27;  // longer keys (beyond any batch in HBM) stay sequential
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
@@ -1668,66 +1668,65 @@ __device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, 
 // the parts of a key of n updates
 __device__ __forceinline__ int64_t spec_parts(int64_t n) { return (n + kSpecLen - 1) / kSpecLen; }
 
-// one block: the keys of >= spec_min updates among the long keys, in
-// long_idx order, with their parts' and work items' running offsets
-__global__ __launch_bounds__(1024) void td_spec_plan_kernel(const int64_t* __restrict__ seg_off,
-                                                            const int64_t* __restrict__ long_idx, int64_t n_long,
-                                                            int64_t spec_min, int64_t* __restrict__ hdr,
+// the keys of >= spec_min updates among the long keys, compacted into the
+// plan (slot order is arbitrary: each key's result is its own) with their
+// part counts; hdr[3] counts them (zeroed by the launcher)
+__global__ __launch_bounds__(kBlock) void td_spec_select_kernel(const int64_t* __restrict__ seg_off,
+                                                                const int64_t* __restrict__ long_idx, int64_t n_long,
+                                                                int64_t spec_min, int64_t* __restrict__ hdr,
+                                                                SpecPlanEntry* __restrict__ plan) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= n_long) return;
+    const int64_t s = long_idx[k], n = seg_off[s + 1] - seg_off[s];
+    if (n < spec_min || n > kSpecMaxLen) return;
+    const int64_t slot = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 3), 1ull);
+    plan[slot] = SpecPlanEntry{s, 0, 0, spec_parts(n)};
+}
+// one block: the running offsets of the selected keys' parts and work items
+// (exclusive scans over the plan), and the totals into hdr[0..2]
+__global__ __launch_bounds__(1024) void td_spec_plan_kernel(int64_t* __restrict__ hdr,
                                                             SpecPlanEntry* __restrict__ plan) {
-    __shared__ u32 wsum[3][16];
-    __shared__ int64_t carry[3];
+    __shared__ u32 wsum[2][16];
+    __shared__ int64_t carry[2];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t < 3) carry[t] = 0;
+    const int64_t n_spec = hdr[3];
+    if (t < 2) carry[t] = 0;
     __syncthreads();
-    // kPlanBatch tiles of 1,024 keys at a time: their loads all issued before
-    // the first is used (two dependent round trips per batch, not per tile)
-    constexpr int kPlanBatch = 8;
-    for (int64_t b0 = 0; b0 < n_long; b0 += 1024 * kPlanBatch) {
-      int64_t sb[kPlanBatch], lo[kPlanBatch], hi[kPlanBatch];
+    for (int64_t t0 = 0; t0 < n_spec; t0 += 1024) {
+        const int64_t k = t0 + t;
+        const u32 P = k < n_spec ? (u32)plan[k].n_parts : 0u, C = (P + kSpecLanes - 1) / kSpecLanes;
+        const u32 in[2] = {P, C};
+        u32 incl[2];
 #pragma unroll
-      for (int u = 0; u < kPlanBatch; u++) {
-          const int64_t k = b0 + u * 1024 + t;
-          sb[u] = k < n_long ? long_idx[k] : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < kPlanBatch; u++) {
-          lo[u] = sb[u] >= 0 ? seg_off[sb[u]] : 0;
-          hi[u] = sb[u] >= 0 ? seg_off[sb[u] + 1] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < kPlanBatch; u++) {
-        const int64_t t0 = b0 + u * 1024;
-        if (t0 >= n_long) break;  // block-uniform
-        const int64_t s = sb[u], n = hi[u] - lo[u];
-        const bool f = s >= 0 && n >= spec_min && n <= kSpecMaxLen;
-        const u32 P = f ? (u32)spec_parts(n) : 0u, C = (P + kSpecLanes - 1) / kSpecLanes;
-        // block-wide exclusive scans of (f, P, C): lanes by DPP, waves through LDS
-        const u32 in[3] = {f ? 1u : 0u, P, C};
-        u32 incl[3];
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
+        for (int c = 0; c < 2; c++) {
             incl[c] = wave_incl_scan(in[c]);
             if (lane == 63) wsum[c][wv] = incl[c];
         }
         __syncthreads();
-        int64_t ex[3];
+        int64_t ex[2];
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
+        for (int c = 0; c < 2; c++) {
             u32 before = 0;
             for (int w2 = 0; w2 < wv; w2++) before += wsum[c][w2];
             ex[c] = carry[c] + before + incl[c] - in[c];
         }
-        if (f) plan[ex[0]] = SpecPlanEntry{s, ex[1], ex[2], (int64_t)P};
+        if (k < n_spec) {
+            plan[k].part_base = ex[0];
+            plan[k].item_base = ex[1];
+        }
         __syncthreads();
-        if (t < 3) {
+        if (t < 2) {
             u32 tot = 0;
             for (int w2 = 0; w2 < 16; w2++) tot += wsum[t][w2];
             carry[t] += tot;
         }
         __syncthreads();
-      }
     }
-    if (t < 3) hdr[t] = carry[t];
+    if (t == 0) {
+        hdr[0] = n_spec;
+        hdr[1] = carry[1];
+        hdr[2] = carry[0];
+    }
 }
 // the key of work item w: the last plan entry whose first item is <= w
 __device__ __forceinline__ int64_t spec_key_of(const SpecPlanEntry* plan, int64_t n_spec, int64_t w) {
@@ -2251,17 +2250,20 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
     return launched();
 }
 
-// warm-up length of td_ema_spec_kernel for the rule's contraction |1 - a|:
-// the smallest w with |1 - a|^w < 2^-64; 0 (no speculation) when the rule
-// does not contract or w would pass 2^20.  OTH_TD_SPEC_WARM overrides it
-// (tools/tests only: a tiny warm-up makes the guesses miss, which exercises
-// the rerun path).
+// warm-up length of the split's guesses for the rule's contraction |1 - a|:
+// 4/3 of the smallest w with |1 - a|^w < 2^-64 (at w itself the two runs are
+// still one ulp apart now and then: 4 misses among the first 40 split keys of
+// a 262,144-game batch at a = 0.03; none at 4/3 w, and the reruns cost more
+// than the longer warm-ups: tools/diag/td_spec_probe.py); 0 (no speculation)
+// when the rule does not contract or w would pass 2^20.  OTH_TD_SPEC_WARM
+// overrides it (tools/tests only: a tiny warm-up makes the guesses miss,
+// which exercises the rerun passes).
 static int64_t td_spec_warm(double oma) {
     if (const char* env = getenv("OTH_TD_SPEC_WARM")) return atoll(env);
     const double c = fabs(oma);
     if (!(c < 1.0)) return 0;
     if (c == 0.0) return 1;
-    const double w = ceil(-64.0 * log(2.0) / log(c));
+    const double w = ceil(-64.0 * log(2.0) / log(c) * 4.0 / 3.0);
     return w > (double)(1 << 20) ? 0 : (int64_t)w;
 }
 
@@ -2298,7 +2300,13 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     const int64_t parts = n_values / kSpecLen + n_long + 1;
     double* fin = guess + parts;
     const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
-    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long, 4 * warm, hdr, plan);
+    const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, (hipStream_t)stream);
+    if (me != hipSuccess) return status(me);
+    td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long,
+                                                                                    4 * warm, hdr, plan);
+    rc = launched();
+    if (rc != OTH_OK) return rc;
+    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan);
     rc = launched();
     if (rc != OTH_OK) return rc;
     const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);

@@ -106,9 +106,10 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
 
 @pytest.mark.parametrize("kind", ["normal", "constant", "sparse"])
 def test_td_ema_split_speculation_learner_rate(kind):
-    """Long segments at the learner's rate (a = 0.03, warm-up 1457 values) split
-    over up to 512 lanes (600,001 values: 512 parts of 1,184): the result is the
-    sequential rule's, bit for bit,
+    """Long segments at the learner's rate (a = 0.03, warm-up 1,942 values: 4/3
+    of the 2^-64 contraction length) split into parts of 1,040 (600,001 values:
+    577 parts over 10 one-wave work items; 7,767 values stay on one lane, 7,768
+    are split): the result is the sequential rule's, bit for bit,
     whether the lanes' guesses converge (random targets), sit on a fixed
     point of the rounding (a constant target) or run through exact zeros
     (mostly-zero targets: draws)."""
@@ -116,7 +117,7 @@ def test_td_ema_split_speculation_learner_rate(kind):
     a = 0.03
     oma = 1 - a
     rng = np.random.default_rng({"normal": 5, "constant": 6, "sparse": 7}[kind])
-    lengths = [5827, 5828, 9000, 70001, 200003, 600001]
+    lengths = [7767, 7768, 9000, 70001, 200003, 600001]
     vals, seg, want = [], [0], []
     for L in lengths:
         if kind == "normal":

@@ -40,7 +40,7 @@ for k in range(2):
     sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
 torch.cuda.synchronize()
 a, oma = sm.a, 1 - sm.a
-warm = int(os.environ.get("OTH_TD_SPEC_WARM", 0)) or math.ceil(-64 * math.log(2) / math.log(abs(oma)))
+warm = int(os.environ.get("OTH_TD_SPEC_WARM", 0)) or math.ceil(-64 * math.log(2) / math.log(abs(oma)) * 4 / 3)
 warm16 = (warm + 15) // 16 * 16
 sk, sv = cap["sk"], cap["sv"]
 ukeys, counts = torch.unique_consecutive(sk, return_counts=True)

@@ -534,19 +534,26 @@ def _bench_step_graph(ops, torch, dev, args, n=65536, launches=200):
             "us_per_launch": dt / launches * 1e6}
 
 
-def _bench_sharded(torch, args, policy, steps=10, reps=3):
+def _bench_sharded(torch, args, policy, steps=10, reps=5):
     """The product's multi-GPU entry as a single-process caller uses it:
-    dist.rollout_sharded(steps * games, steps=steps) -- `steps` launches of
-    `games` games pipelined on two streams (ops.rollout_batches) -- timed by
-    the host clock around the call and a device sync (median of `reps`)."""
+    dist.rollout_sharded(steps * games, steps=steps) -- `steps` batches of
+    `games` games (ops.rollout_batches: merged into launches of up to
+    ops.ROLLOUT_MERGE_GAMES, round-robin on the streams) -- timed by the host
+    clock around the call and a device sync (median of `reps`, after ~0.3 s
+    of the same calls so that the clock has ramped, as for the headline)."""
     from subproc_amd.dist import rollout_sharded
+    from subproc_amd.ops import ROLLOUT_MERGE_GAMES
 
     n = args.games
-    rollout_sharded(2 * n, args.seed, policy, steps=2, game_id_base=1 << 45)  # first-use warm-up
-    torch.cuda.synchronize()
-    out = {"metric": "env-steps/sec (dist.rollout_sharded, %d pipelined launches of %d games, one process)"
-                     % (steps, n), "unit": "env-steps/s", "policy": policy}
-    for streams in (2, 3):
+    t_end = time.perf_counter() + args.prewarm_ms * 1e-3
+    while True:  # first use, then the clock ramp
+        rollout_sharded(steps * n, args.seed, policy, steps=steps, game_id_base=1 << 45)
+        torch.cuda.synchronize()
+        if time.perf_counter() >= t_end:
+            break
+    out = {"metric": "env-steps/sec (dist.rollout_sharded, %d batches of %d games, one process)" % (steps, n),
+           "unit": "env-steps/s", "policy": policy, "merge_games": ROLLOUT_MERGE_GAMES}
+    for streams in (2,):
         rates, gpu_rates = [], []
         for r in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -273,19 +273,25 @@ def _side_streams(d, k):
     return have[:k]
 
 
+ROLLOUT_MERGE_GAMES = 1 << 24  # rollout_batches merges batches into launches of up to this many games
+
+
 def rollout_batches(n, steps, seed, game_id0=0, policy="random", n_random=10, hist=None, device="cuda", streams=2,
-                    want_boards=False, want_diff=False, want_plies=False, weights=None):
-    """`steps` back-to-back rollout launches of `n` games each, pipelined:
-    launch s plays global ids [game_id0 + s*n, +n) and the launches are issued
-    round-robin on `streams` HIP streams (torch's current stream and
-    streams - 1 side streams, each with its own work word), so the last
-    batches of one launch share the CUs with the first batches of the next
-    instead of leaving them idle (batch tail).  The result
-    equals ``rollout(n * steps, seed, game_id0, ...)`` game for game: every
-    game keeps the RNG stream of its global id, and the launches add into one
-    histogram (device atomics).  Outputs, if asked for, are (n * steps, ...)
-    in game-id order.  On return the current stream is ordered after every
-    launch; nothing is synchronised with the host.
+                    want_boards=False, want_diff=False, want_plies=False, weights=None, merge=True):
+    """`steps` batches of `n` games each, pipelined: batch s plays global ids
+    [game_id0 + s*n, +n).  Consecutive batches are merged into launches of up
+    to max(n, ROLLOUT_MERGE_GAMES) games (merge=False: one launch per batch),
+    and the launches are issued round-robin on `streams` HIP streams (torch's
+    current stream and streams - 1 side streams, each with its own work
+    word), so the last batches of one launch share the CUs with the first
+    batches of the next instead of leaving them idle (batch
+    tail): ten batches of 1M games run as one launch of 10M, with one launch
+    tail where ten launches had ten.  The result equals ``rollout(n * steps, seed, game_id0,
+    ...)`` game for game whatever the launches: every game keeps the RNG
+    stream of its global id, and the launches add into one histogram (device
+    atomics).  Outputs, if asked for, are (n * steps, ...) in game-id order.
+    On return the current stream is ordered after every launch; nothing is
+    synchronised with the host.
     """
     if policy not in _POLICIES:
         raise ValueError(f"policy must be 'random', 'greedy' or 'eval', got {policy!r}")
@@ -320,23 +326,27 @@ def rollout_batches(n, steps, seed, game_id0=0, policy="random", n_random=10, hi
         for st in sts:
             with torch.cuda.stream(st):
                 works.append(work_word(d))
-        for s in range(steps):
-            i = s % len(sts)
+        per = 1  # batches per launch
+        if merge and n > 0:
+            per = max(1, min(steps, ROLLOUT_MERGE_GAMES // n))
+        for L, s0 in enumerate(range(0, steps, per)):
+            i = L % len(sts)
             st, w = sts[i], works[i]
-            g0 = game_id0 + s * n
+            g0 = game_id0 + s0 * n
+            m = min(per, steps - s0) * n  # this launch's games
 
             def part(t, k=1):
-                return None if t is None else t.data_ptr() + s * n * k * t.element_size()
+                return None if t is None else t.data_ptr() + s0 * n * k * t.element_size()
 
             if pid == POLICY_EVAL:
                 rc = lib.oth_rollout_eval(None, None, seed & (2**64 - 1), g0, n_random, wp, part(fb, 2), part(df),
-                                          part(pl), None, ph, w.data_ptr(), n, st.cuda_stream)
+                                          part(pl), None, ph, w.data_ptr(), m, st.cuda_stream)
             else:
                 rc = lib.oth_rollout(None, None, seed & (2**64 - 1), g0, pid, n_random, part(fb, 2), part(df),
-                                     part(pl), None, ph, w.data_ptr(), n, st.cuda_stream)
+                                     part(pl), None, ph, w.data_ptr(), m, st.cuda_stream)
             if rc != _lib.OTH_OK:  # the failed launch's word is unknown: drop it (ops.rollout does the same)
                 _WORK.pop((d.index, st.cuda_stream), None)
-            check(rc, "oth_rollout (rollout_batches step %d)" % s)
+            check(rc, "oth_rollout (rollout_batches launch %d)" % L)
         for st in side:  # the caller's stream waits for every launch
             e = torch.cuda.Event()
             e.record(st)

@@ -53,15 +53,20 @@ def test_two_ranks_on_one_gpu_equal_one_process(policy, steps):
         np.testing.assert_array_equal(out[rank][0], ref)
 
 
-@pytest.mark.parametrize("policy,streams", [("random", 2), ("random", 3), ("greedy", 2), ("eval", 1)])
-def test_rollout_batches_equal_one_launch(policy, streams):
-    """ops.rollout_batches: K pipelined launches == one launch over the same
-    global ids, game for game (final boards, diff, plies) and histogram."""
+@pytest.mark.parametrize("policy,streams,merge", [("random", 2, True), ("random", 2, False), ("random", 3, True),
+                                                  ("greedy", 2, True), ("greedy", 3, False), ("eval", 1, True)])
+def test_rollout_batches_equal_one_launch(policy, streams, merge, monkeypatch):
+    """ops.rollout_batches: K pipelined batches == one launch over the same
+    global ids, game for game (final boards, diff, plies) and histogram, with
+    the batches merged into launches of up to ops.ROLLOUT_MERGE_GAMES games
+    (here set so that 5 batches run as launches of 2, 2 and 1 batches) or one
+    launch each."""
     from subproc_amd import ops
 
     n, K, seed, g0 = 40_009, 5, 0x5EED, (1 << 36) + 11
+    monkeypatch.setattr(ops, "ROLLOUT_MERGE_GAMES", 2 * n + 5)
     a = ops.rollout_batches(n, K, seed, g0, policy, 10, device="cuda:0", streams=streams, want_boards=True,
-                            want_diff=True, want_plies=True)
+                            want_diff=True, want_plies=True, merge=merge)
     b = ops.rollout(n * K, seed, g0, policy, 10, device="cuda:0")
     torch.cuda.synchronize()
     assert torch.equal(a.final_boards, b.final_boards)

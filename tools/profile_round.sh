@@ -10,7 +10,7 @@ O=gpurun_out/prof_$R
 mkdir -p $O
 # no time-based pre-warm (single-stream launches) in profiled runs: every launch of
 # the headline kernel is then a two-stream bench step, as in the bench line
-BENCH="bench.py --steps 100 --warmup 100 --prewarm-ms 0"
+BENCH="bench.py --steps 100 --warmup 100 --prewarm-ms 0 --cpu-games 2000"
 # rollout_16M, rollout_1stream and rollout_sharded share the headline kernel and grid: keep them
 # out of the per-launch averages
 export BENCH_SKIP=rollout_16M,rollout_1stream,rollout_sharded

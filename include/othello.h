@@ -335,6 +335,19 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
  * oth_td_sort_pairs. */
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream);
+/* The segments of a key-sorted update stream (what StateMap.update groups
+ * by): counts[0] = n_seg, the number of distinct keys; seg_off[0..n_seg] the
+ * offsets of their runs (seg_off[j] = first index of key j, seg_off[n_seg]
+ * = n); ukeys[0..n_seg) the keys; long_idx[0..counts[1]) the indices j of
+ * the segments of >= long_min updates, in no particular order (what
+ * oth_td_ema_split takes).  seg_off holds n + 1 entries, ukeys and long_idx
+ * n (capacities: the counts are known only after the call); counts (2
+ * int64) is device memory, like the rest.  temp / temp_bytes as
+ * oth_td_sort_pairs.  Replaces torch's unique_consecutive + cumsum +
+ * nonzero (and their two host syncs). */
+int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
+                    int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream);
+
 /* Packed words -> keys[i] = the word's low OTH_TD_KEY_BITS and values[i] =
  * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device). */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,

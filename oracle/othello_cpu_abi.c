@@ -349,6 +349,31 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
 }
 
+/* the segments of a key-sorted stream: starts in order, long ones in order
+   (the GPU lists those in any order) */
+int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
+                    int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream) {
+    (void)stream;
+    if (n < 0 || long_min < 1 || !temp_bytes) return OTH_EINVAL;
+    if (!temp) {
+        *temp_bytes = 0;
+        return OTH_OK;
+    }
+    if (!seg_off || !counts || (n > 0 && (!keys || !ukeys || !long_idx))) return OTH_EINVAL;
+    int64_t m = 0, nl = 0;
+    for (int64_t i = 0; i < n; i++)
+        if (i == 0 || keys[i] != keys[i - 1]) {
+            seg_off[m] = i;
+            ukeys[m++] = keys[i];
+        }
+    seg_off[m] = n;
+    for (int64_t j = 0; j < m; j++)
+        if (seg_off[j + 1] - seg_off[j] >= long_min) long_idx[nl++] = j;
+    counts[0] = m;
+    counts[1] = nl;
+    return OTH_OK;
+}
+
 /* stable sort of (key, value) pairs by key: bottom-up merge sort of the pair
  * indices (temp holds 2 * n int64 indices), then a gather */
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,

@@ -97,10 +97,24 @@ __device__ __forceinline__ void eval_weights_to_lds(const EvalWeights& ew, int* 
     }
 }
 // sum_j w[j] * counts()[1+j] for the side owning `mine`, with mobility `mob`
+// The products by 24-bit multiplies (v_mul_i32_i24, full rate) where a plain
+// int multiply is v_mul_lo_u32, a multi-pass instruction: the weights are
+// int8 and the counts <= 64, so every product and partial sum is exact in
+// 24 bits.  OTH_EVAL_MUL24=0: A/B builds only.
+#ifndef OTH_EVAL_MUL24
+#define OTH_EVAL_MUL24 1
+#endif
+__device__ __forceinline__ int eval_mul(int w, int c) {
+#if OTH_EVAL_MUL24
+    return __mul24(w, c);
+#else
+    return w * c;
+#endif
+}
 __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
-    int v = w[0] * (int)__popcll(mob);
+    int v = eval_mul(w[0], (int)__popcll(mob));
 #pragma unroll
-    for (int k = 0; k < 8; k++) v += w[1 + k] * (int)__popcll(and2(mine, kRegionMasks[k]));
+    for (int k = 0; k < 8; k++) v += eval_mul(w[1 + k], (int)__popcll(and2(mine, kRegionMasks[k])));
     return v;
 }
 

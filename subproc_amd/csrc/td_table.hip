@@ -337,6 +337,96 @@ hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t 
 }
 // the split table's bytes for n merged positions in tiles of `tile` (0 when
 // nothing is merged)
+// ---- segments of the key-sorted update stream (oth_td_segments): where
+// torch's unique_consecutive + cumsum + nonzero took ~0.37 ms per 32M
+// updates (a reduce-by-key, a scan, a partition and their fills, and two
+// host syncs), one wave streams 1,024 keys in 16 coalesced rounds of 64: a
+// segment starts where a key differs from the one before (the lane's
+// neighbour by a DPP shift, the round's first from the round before), a
+// ballot and mbcnt place the starts.  A count pass and a write pass around a
+// scan of the waves' counts keep the order; the long segments are listed by
+// atomic appends, in no particular order (their consumers take any order).
+constexpr int kSegRounds = 16;
+constexpr int kSegWaveKeys = 64 * kSegRounds;
+constexpr int kSegBlock = 256;
+constexpr int kSegWavesPerBlock = kSegBlock / 64;
+template <bool WRITE>
+__global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __restrict__ keys, int64_t n,
+                                                           int64_t* __restrict__ wave_cnt,
+                                                           int64_t* __restrict__ seg_off,
+                                                           int64_t* __restrict__ ukeys) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t base = w * kSegWaveKeys;
+    if (base >= n) return;  // wave-uniform
+    int64_t prev_last = base > 0 ? keys[base - 1] : 0;
+    int64_t pos = WRITE ? wave_cnt[w] : 0;  // the wave's first segment index (after the scan)
+    int64_t cnt = 0;
+#pragma unroll 4
+    for (int r = 0; r < kSegRounds; r++) {
+        const int64_t i = base + r * 64 + lane;
+        const bool in = i < n;
+        const int64_t k = in ? keys[i] : 0;
+        int64_t before = __shfl_up(k, 1);
+        if (lane == 0) before = prev_last;
+        const bool start = in && (i == 0 || k != before);
+        const uint64_t m = __ballot(start);
+        if (WRITE && start) {
+            const int64_t at = pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            seg_off[at] = i;
+            ukeys[at] = k;
+        }
+        pos += __popcll(m);
+        cnt += __popcll(m);
+        prev_last = __shfl(k, 63);
+    }
+    if (!WRITE && lane == 0) wave_cnt[w] = cnt;
+}
+// one block: exclusive scan of the waves' counts in place, the total into
+// counts[0], seg_off[total] = n, counts[1] (the long segments' counter) = 0
+__global__ __launch_bounds__(1024) void td_seg_scan_kernel(int64_t* __restrict__ wave_cnt, int64_t n_waves, int64_t n,
+                                                           int64_t* __restrict__ seg_off,
+                                                           int64_t* __restrict__ counts) {
+    __shared__ int64_t part[1024];
+    __shared__ int64_t carry;
+    const int t = threadIdx.x;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (int64_t t0 = 0; t0 < n_waves; t0 += 1024) {
+        const int64_t k = t0 + t;
+        const int64_t v = k < n_waves ? wave_cnt[k] : 0;
+        part[t] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+            const int64_t add = t >= o ? part[t - o] : 0;
+            __syncthreads();
+            part[t] += add;
+            __syncthreads();
+        }
+        if (k < n_waves) wave_cnt[k] = carry + part[t] - v;
+        __syncthreads();
+        if (t == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (t == 0) {
+        counts[0] = carry;
+        counts[1] = 0;
+        seg_off[carry] = n;
+    }
+}
+// the segments of >= long_min updates, appended in any order
+__global__ __launch_bounds__(kSegBlock) void td_seg_long_kernel(const int64_t* __restrict__ seg_off,
+                                                                int64_t long_min, int64_t* __restrict__ long_idx,
+                                                                int64_t* __restrict__ counts) {
+    const int64_t n_seg = counts[0];
+    for (int64_t j = (int64_t)blockIdx.x * kSegBlock + threadIdx.x; j < n_seg; j += (int64_t)gridDim.x * kSegBlock) {
+        if (seg_off[j + 1] - seg_off[j] >= long_min) {
+            const int64_t at = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), 1ull);
+            long_idx[at] = j;
+        }
+    }
+}
+
 size_t split_bytes(int64_t n_old, int64_t n_upd, int64_t tile) {
     if (n_upd <= 0) return 0;
     return (size_t)((n_old + n_upd + tile - 1) / tile + 1) * sizeof(int64_t);
@@ -428,6 +518,30 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     size_t bytes = *temp_bytes;
     const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
                                                               0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
+                    int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream) {
+    if (n < 0 || long_min < 1 || !temp_bytes) return OTH_EINVAL;
+    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys;
+    const size_t need = (size_t)(n_waves > 0 ? n_waves : 1) * sizeof(int64_t);
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (!seg_off || !counts || (n > 0 && (!keys || !ukeys || !long_idx)) || *temp_bytes < need) return OTH_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    int64_t* wave_cnt = static_cast<int64_t*>(temp);
+    const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
+    if (n > 0) td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys);
+    td_seg_scan_kernel<<<1, 1024, 0, st>>>(wave_cnt, n_waves, n, seg_off, counts);
+    if (n > 0) {
+        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys);
+        const int64_t lb = std::min<int64_t>((n + kSegBlock - 1) / kSegBlock, 2048);
+        td_seg_long_kernel<<<(unsigned)lb, kSegBlock, 0, st>>>(seg_off, long_min, long_idx, counts);
+    }
+    const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 

@@ -225,10 +225,18 @@ class StateMap:
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            ukeys, counts = torch.unique_consecutive(sk, return_counts=True)
-            seg_off = torch.zeros(ukeys.numel() + 1, dtype=torch.int64, device=self.device)
-            torch.cumsum(counts, 0, out=seg_off[1:])
-            n_upd = ukeys.numel()
+            # the stream's segments (keys, run offsets, the long ones) in one
+            # pass pair and one host sync (oth_td_segments)
+            n = sk.numel()
+            seg_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+            ukeys = torch.empty(n, dtype=torch.int64, device=self.device)
+            long_idx = torch.empty(n, dtype=torch.int64, device=self.device)
+            cnt = torch.empty(2, dtype=torch.int64, device=self.device)
+            _with_scratch(lib.oth_td_segments, (sk.data_ptr(), n, LONG_MIN, seg_off.data_ptr(), ukeys.data_ptr(),
+                                                long_idx.data_ptr(), cnt.data_ptr()), stream, self.device,
+                          "oth_td_segments")
+            n_upd, n_long = cnt.tolist()
+            ukeys, seg_off, long_idx = ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
             is_new = None
             if len(self):
                 init = torch.empty(n_upd, dtype=torch.float64, device=self.device)
@@ -240,14 +248,14 @@ class StateMap:
                 init = torch.zeros(n_upd, dtype=torch.float64, device=self.device)
             out = torch.empty_like(init)
             # keys with many updates (the opening and the first plies of every
-            # game) are each run by a whole wavefront (oth_td_ema_split)
-            long_idx = torch.nonzero(counts >= LONG_MIN).flatten()
+            # game) are each run by a whole wavefront, the longest split into
+            # parts over many (oth_td_ema_split)
             _with_scratch(lib.oth_td_ema_split, (sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a,
                                                  1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN,
                                                  long_idx.data_ptr(), long_idx.numel(), sv.numel()),
                           stream, self.device, "oth_td_ema_split")
-            if is_new is None:
-                self.keys, self.values = ukeys, out
+            if is_new is None:  # (a copy: ukeys is a view of an n-entry buffer)
+                self.keys, self.values = ukeys.clone(), out
             else:
                 self._merge(is_new, ukeys, out, lib, stream)
 

@@ -386,6 +386,34 @@ def test_td_pair():
     np.testing.assert_array_equal(out2.h, out.h)
 
 
+def test_td_segments_pair():
+    """oth_td_segments: the runs of a key-sorted stream (short, long, a
+    single-key stream's one run, runs crossing the GPU's 64-key rounds and
+    1,024-key waves) -- offsets and keys equal on both builds and to numpy's,
+    the long segments the same set."""
+    rng = np.random.default_rng(12)
+    for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 1023, 1024, 1025, 5000],
+                                                                          400)):
+        keys = np.repeat(np.cumsum(rng.integers(1, 1000, len(lens))).astype(np.int64), lens)
+        n = len(keys)
+        k = Buf(keys)
+        off, uk, li, cnt = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.int64)),
+                            Buf(np.zeros(2, np.int64)))
+        both_scratch("oth_td_segments", k, n, 48, off, uk, li, cnt)
+        same(cnt)
+        m, nl = (int(x) for x in cnt.h)
+        starts = np.flatnonzero(np.r_[True, keys[1:] != keys[:-1]])
+        assert m == len(starts)
+        np.testing.assert_array_equal(off.h[:m + 1], np.r_[starts, n])
+        np.testing.assert_array_equal(uk.h[:m], keys[starts])
+        np.testing.assert_array_equal(off.d.cpu().numpy()[:m + 1], off.h[:m + 1])
+        np.testing.assert_array_equal(uk.d.cpu().numpy()[:m], uk.h[:m])
+        want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
+        assert nl == len(want)
+        np.testing.assert_array_equal(li.h[:nl], want)
+        np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
+
+
 def test_empty_null_and_invalid_arguments():
     """n = 0 is a no-op for every entry point; optional outputs may be NULL;
     bad arguments return OTH_EINVAL before anything is launched (both builds)."""

@@ -348,6 +348,12 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
                     int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream);
 
+/* new_before[j] = the number of nonzero is_new[0..j) for j = 0..n (n + 1
+ * entries, device): oth_td_merge's new_before from oth_td_lookup's is_new.
+ * temp / temp_bytes as oth_td_sort_pairs. */
+int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
+                      void* stream);
+
 /* Packed words -> keys[i] = the word's low OTH_TD_KEY_BITS and values[i] =
  * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device). */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,

@@ -349,6 +349,24 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
 }
 
+int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
+                      void* stream) {
+    (void)stream;
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    if (!temp) {
+        *temp_bytes = 0;
+        return OTH_OK;
+    }
+    if (!new_before || (n > 0 && !is_new)) return OTH_EINVAL;
+    int64_t c = 0;
+    for (int64_t j = 0; j < n; j++) {
+        new_before[j] = c;
+        c += is_new[j] != 0;
+    }
+    new_before[n] = c;
+    return OTH_OK;
+}
+
 /* the segments of a key-sorted stream: starts in order, long ones in order
    (the GPU lists those in any order) */
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,

@@ -49,6 +49,7 @@ SIGNATURES = {
     "oth_td_updates_rows": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_updates_records": (_I, [_P, _P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),
+    "oth_td_new_before": (_I, [_P, _I64, _P, _P, _P, _P]),
     "oth_td_segments": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "oth_td_ema_split": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64, _I64, _P, _P,
                               _P]),

@@ -109,6 +109,10 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
                                                                double* __restrict__ out_v) {
     __shared__ int64_t sk[kMergeTile];
     __shared__ double sv[kMergeTile];
+    // the hits before each of the tile's batch keys, relative to its first:
+    // hits_before(b0 + k) = hits0 + shits[k] (the merge loop's per-output
+    // new_before reads from LDS, not from global memory: round 4)
+    __shared__ int shits[kMergeTile + 1];
     __shared__ unsigned long long range[2];  // min slot, max slot + 1 of the block's outputs
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
@@ -128,6 +132,8 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
         sk[na + k] = B[b0 + k];
         sv[na + k] = Bv[b0 + k];
     }
+    const int64_t hits0 = b0 - new_before[b0];
+    for (int k = tid; k <= nb; k += kMergeBlock) shits[k] = (int)((b0 + k - new_before[b0 + k]) - hits0);
     __syncthreads();
     const int n = na + nb;
     const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
@@ -154,16 +160,14 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
         if (i < na && (j >= nb || sk[i] < sk[na + j])) {
             const int64_t key = sk[i];
             if (key != prev_b) {  // not the table copy of the batch key just taken
-                const int64_t bc = b0 + j;
-                os[q] = (uint64_t)(gm - (bc - new_before[bc]));
+                os[q] = (uint64_t)(gm - (hits0 + shits[j]));
                 ok[q] = key;
                 ov[q] = sv[i];
             }
             i++;
         } else {
-            const int64_t bj = b0 + j;
             const int64_t key = sk[na + j];
-            os[q] = (uint64_t)(gm - (bj - new_before[bj]));
+            os[q] = (uint64_t)(gm - (hits0 + shits[j]));
             ok[q] = key;
             ov[q] = sv[na + j];
             prev_b = key;
@@ -210,8 +214,7 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
                                                                 double* __restrict__ init,
                                                                 uint8_t* __restrict__ is_new) {
     __shared__ int64_t sk[kLookupTile];
-    __shared__ double sinit[kLookupTile];
-    __shared__ uint8_t snew[kLookupTile];
+    __shared__ int shit[kLookupTile];  // a batch key's table entry relative to a0, or -1 (not in the table)
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kLookupTile;
     const int64_t d1 = d0 + kLookupTile < nA + nB ? d0 + kLookupTile : nA + nB;
@@ -238,15 +241,16 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
         // batch key b0 + j; the next table key is A[a0 + i] (past the tile: from HBM)
         const int64_t key = sk[na + j], ai = a0 + i;
         const int64_t next = i < na ? sk[i] : (ai < nA ? A[ai] : -1);
-        const bool hit = next == key;
-        sinit[j] = hit ? Av[ai] : 0.0;
-        snew[j] = hit ? 0 : 1;
+        shit[j] = next == key ? i : -1;
         j++;
     }
     __syncthreads();
+    // the hits' values loaded here, all in flight at once, not one per step of
+    // the merge loop above (round 4)
     for (int k = tid; k < nb; k += kMergeBlock) {
-        init[b0 + k] = sinit[k];
-        is_new[b0 + k] = snew[k];
+        const int r = shit[k];
+        init[b0 + k] = r >= 0 ? Av[a0 + r] : 0.0;
+        is_new[b0 + k] = r >= 0 ? 0 : 1;
     }
 }
 
@@ -381,6 +385,28 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         prev_last = __shfl(k, 63);
     }
     if (!WRITE && lane == 0) wave_cnt[w] = cnt;
+}
+// the exclusive running count of is_new (oth_td_new_before), the same two
+// passes: per wave a count, then, after the scan, every position's count
+template <bool WRITE>
+__global__ __launch_bounds__(kSegBlock) void td_count_kernel(const uint8_t* __restrict__ flags, int64_t n,
+                                                             int64_t* __restrict__ wave_cnt,
+                                                             int64_t* __restrict__ before) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t base = w * kSegWaveKeys;
+    if (base >= n) return;  // wave-uniform
+    int64_t pos = WRITE ? wave_cnt[w] : 0;
+#pragma unroll 4
+    for (int r = 0; r < kSegRounds; r++) {
+        const int64_t i = base + r * 64 + lane;
+        const bool set = i < n && flags[i] != 0;
+        const uint64_t m = __ballot(set);
+        if (WRITE && i < n)
+            before[i] = pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        pos += __popcll(m);
+    }
+    if (!WRITE && lane == 0) wave_cnt[w] = pos;
 }
 // one block: exclusive scan of the waves' counts in place, the total into
 // counts[0], seg_off[total] = n, counts[1] (the long segments' counter) = 0
@@ -542,6 +568,31 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
         td_seg_long_kernel<<<(unsigned)lb, kSegBlock, 0, st>>>(seg_off, long_min, long_idx, counts);
     }
     const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
+                      void* stream) {
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys;
+    const size_t need = (size_t)(n_waves > 0 ? n_waves : 1) * sizeof(int64_t) + 2 * sizeof(int64_t);
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (!new_before || (n > 0 && !is_new) || *temp_bytes < need) return OTH_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    int64_t* wave_cnt = static_cast<int64_t*>(temp);
+    int64_t* counts = wave_cnt + (n_waves > 0 ? n_waves : 1);  // the scan kernel's [total, 0]
+    const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
+    if (n > 0) td_count_kernel<false><<<blocks, kSegBlock, 0, st>>>(is_new, n, wave_cnt, new_before);
+    // (the scan writes new_before[total] = n first; the write pass below and
+    // the copy of the total into new_before[n] then overwrite what they own)
+    td_seg_scan_kernel<<<1, 1024, 0, st>>>(wave_cnt, n_waves, n, new_before, counts);
+    if (n > 0) td_count_kernel<true><<<blocks, kSegBlock, 0, st>>>(is_new, n, wave_cnt, new_before);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(new_before + n, counts, sizeof(int64_t), hipMemcpyDeviceToDevice, st);
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 

@@ -265,8 +265,9 @@ class StateMap:
         union, placing every element by rank; new_before[j] = batch keys
         before j that are new."""
         n_old, n_upd = len(self), ukeys.numel()
-        new_before = torch.zeros(n_upd + 1, dtype=torch.int64, device=self.device)
-        torch.cumsum(is_new, 0, out=new_before[1:])
+        new_before = torch.empty(n_upd + 1, dtype=torch.int64, device=self.device)
+        _with_scratch(lib.oth_td_new_before, (is_new.data_ptr(), n_upd, new_before.data_ptr()), stream, self.device,
+                      "oth_td_new_before")
         n_new = int(new_before[-1])
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)

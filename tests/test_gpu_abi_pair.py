@@ -414,6 +414,20 @@ def test_td_segments_pair():
         np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
 
 
+def test_td_new_before_pair():
+    """oth_td_new_before: the running count of a byte flag array (empty, short,
+    across the GPU's 64-flag rounds and 1,024-flag waves), equal on both builds
+    and to numpy's."""
+    rng = np.random.default_rng(13)
+    for n in (0, 1, 63, 64, 65, 1023, 1024, 1025, 200_003):
+        f = (rng.random(n) < 0.4).astype(np.uint8) * rng.integers(1, 255, n).astype(np.uint8)
+        fl = Buf(f if n else np.zeros(1, np.uint8))
+        nb = Buf(np.zeros(n + 1, np.int64))
+        both_scratch("oth_td_new_before", fl, n, nb)
+        same(nb)
+        np.testing.assert_array_equal(nb.h, np.r_[0, np.cumsum(f[:n] != 0)])
+
+
 def test_empty_null_and_invalid_arguments():
     """n = 0 is a no-op for every entry point; optional outputs may be NULL;
     bad arguments return OTH_EINVAL before anything is launched (both builds)."""

@@ -1619,6 +1619,10 @@ struct SpecPlanEntry {
 };
 constexpr int kSpecHdr = 8;  // int64 header of the scratch: [0] keys split, [1] work items, [2] parts, [3] counter
 constexpr int64_t kSpecMaxLen = 1ll << 27;  // longer keys (beyond any batch in HBM) stay sequential
+// keys of >= 3 warm-ups are split (at a = 0.03: 5,826 updates, the single-lane
+// chain's longest as in round 3; at 4 warm-ups of the longer round-4 warm-up,
+// 7,768, the long-key kernel took 199 us against 130)
+constexpr int64_t kSpecMinWarms = 3;
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
@@ -1844,7 +1848,7 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
     const int lane = threadIdx.x;
     const int64_t s = long_idx[blockIdx.x];
     const int64_t b = seg_off[s], e = seg_off[s + 1];
-    if (warm > 0 && e - b >= 4 * warm && e - b <= kSpecMaxLen) return;  // a split key (td_spec_*)
+    if (warm > 0 && e - b >= kSpecMinWarms * warm && e - b <= kSpecMaxLen) return;  // a split key (td_spec_*)
     const int64_t n_stage = (e - b + kTdStage - 1) / kTdStage;
     double r[kTdStageLoads];
     auto fetch = [&](int64_t c) {
@@ -2317,7 +2321,7 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, (hipStream_t)stream);
     if (me != hipSuccess) return status(me);
     td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long,
-                                                                                    4 * warm, hdr, plan);
+                                                                                    kSpecMinWarms * warm, hdr, plan);
     rc = launched();
     if (rc != OTH_OK) return rc;
     td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan);

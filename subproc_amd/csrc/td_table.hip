@@ -109,10 +109,6 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
                                                                double* __restrict__ out_v) {
     __shared__ int64_t sk[kMergeTile];
     __shared__ double sv[kMergeTile];
-    // the hits before each of the tile's batch keys, relative to its first:
-    // hits_before(b0 + k) = hits0 + shits[k] (the merge loop's per-output
-    // new_before reads from LDS, not from global memory: round 4)
-    __shared__ int shits[kMergeTile + 1];
     __shared__ unsigned long long range[2];  // min slot, max slot + 1 of the block's outputs
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
@@ -132,8 +128,6 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
         sk[na + k] = B[b0 + k];
         sv[na + k] = Bv[b0 + k];
     }
-    const int64_t hits0 = b0 - new_before[b0];
-    for (int k = tid; k <= nb; k += kMergeBlock) shits[k] = (int)((b0 + k - new_before[b0 + k]) - hits0);
     __syncthreads();
     const int n = na + nb;
     const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
@@ -160,14 +154,16 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
         if (i < na && (j >= nb || sk[i] < sk[na + j])) {
             const int64_t key = sk[i];
             if (key != prev_b) {  // not the table copy of the batch key just taken
-                os[q] = (uint64_t)(gm - (hits0 + shits[j]));
+                const int64_t bc = b0 + j;
+                os[q] = (uint64_t)(gm - (bc - new_before[bc]));
                 ok[q] = key;
                 ov[q] = sv[i];
             }
             i++;
         } else {
+            const int64_t bj = b0 + j;
             const int64_t key = sk[na + j];
-            os[q] = (uint64_t)(gm - (hits0 + shits[j]));
+            os[q] = (uint64_t)(gm - (bj - new_before[bj]));
             ok[q] = key;
             ov[q] = sv[na + j];
             prev_b = key;
@@ -354,37 +350,49 @@ constexpr int kSegRounds = 16;
 constexpr int kSegWaveKeys = 64 * kSegRounds;
 constexpr int kSegBlock = 256;
 constexpr int kSegWavesPerBlock = kSegBlock / 64;
+// WRITE: a segment that starts at i is long iff keys[i + long_min - 1] is
+// its key (the keys are sorted): one more load per start, mostly from the
+// same lines, and an atomic append; no pass of its own over the offsets
 template <bool WRITE>
 __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __restrict__ keys, int64_t n,
                                                            int64_t* __restrict__ wave_cnt,
                                                            int64_t* __restrict__ seg_off,
-                                                           int64_t* __restrict__ ukeys) {
+                                                           int64_t* __restrict__ ukeys, int64_t long_min,
+                                                           int64_t* __restrict__ long_idx,
+                                                           int64_t* __restrict__ counts) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
     const int64_t base = w * kSegWaveKeys;
     if (base >= n) return;  // wave-uniform
-    int64_t prev_last = base > 0 ? keys[base - 1] : 0;
-    int64_t pos = WRITE ? wave_cnt[w] : 0;  // the wave's first segment index (after the scan)
-    int64_t cnt = 0;
-#pragma unroll 4
+    // every round's key loaded before the first is used (16 loads in flight)
+    int64_t k[kSegRounds];
+#pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
-        const bool in = i < n;
-        const int64_t k = in ? keys[i] : 0;
-        int64_t before = __shfl_up(k, 1);
+        k[r] = i < n ? keys[i] : 0;
+    }
+    int64_t prev_last = base > 0 ? keys[base - 1] : 0;
+    int64_t pos = WRITE ? wave_cnt[w] : 0;  // the wave's first segment index (after the scan)
+#pragma unroll
+    for (int r = 0; r < kSegRounds; r++) {
+        const int64_t i = base + r * 64 + lane;
+        int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
-        const bool start = in && (i == 0 || k != before);
+        const bool start = i < n && (i == 0 || k[r] != before);
         const uint64_t m = __ballot(start);
         if (WRITE && start) {
-            const int64_t at = pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const int64_t at =
+                pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             seg_off[at] = i;
-            ukeys[at] = k;
+            ukeys[at] = k[r];
+            const int64_t e = i + long_min - 1;
+            if (e < n && keys[e] == k[r])
+                long_idx[atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), 1ull)] = at;
         }
         pos += __popcll(m);
-        cnt += __popcll(m);
-        prev_last = __shfl(k, 63);
+        prev_last = __shfl(k[r], 63);
     }
-    if (!WRITE && lane == 0) wave_cnt[w] = cnt;
+    if (!WRITE && lane == 0) wave_cnt[w] = pos;
 }
 // the exclusive running count of is_new (oth_td_new_before), the same two
 // passes: per wave a count, then, after the scan, every position's count
@@ -410,49 +418,37 @@ __global__ __launch_bounds__(kSegBlock) void td_count_kernel(const uint8_t* __re
 }
 // one block: exclusive scan of the waves' counts in place, the total into
 // counts[0], seg_off[total] = n, counts[1] (the long segments' counter) = 0
+// (thread t owns the run [t * per, (t + 1) * per) of the counts: its serial
+// sum, a block scan of the 1,024 sums, then its run's prefixes)
 __global__ __launch_bounds__(1024) void td_seg_scan_kernel(int64_t* __restrict__ wave_cnt, int64_t n_waves, int64_t n,
                                                            int64_t* __restrict__ seg_off,
                                                            int64_t* __restrict__ counts) {
     __shared__ int64_t part[1024];
-    __shared__ int64_t carry;
     const int t = threadIdx.x;
-    if (t == 0) carry = 0;
+    const int64_t per = (n_waves + 1023) / 1024;
+    const int64_t b = min<int64_t>(t * per, n_waves), e = min<int64_t>(b + per, n_waves);
+    int64_t sum = 0;
+    for (int64_t k = b; k < e; k++) sum += wave_cnt[k];
+    part[t] = sum;
     __syncthreads();
-    for (int64_t t0 = 0; t0 < n_waves; t0 += 1024) {
-        const int64_t k = t0 + t;
-        const int64_t v = k < n_waves ? wave_cnt[k] : 0;
-        part[t] = v;
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the 1,024 sums
+        const int64_t add = t >= o ? part[t - o] : 0;
         __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-            const int64_t add = t >= o ? part[t - o] : 0;
-            __syncthreads();
-            part[t] += add;
-            __syncthreads();
-        }
-        if (k < n_waves) wave_cnt[k] = carry + part[t] - v;
-        __syncthreads();
-        if (t == 1023) carry += part[1023];
+        part[t] += add;
         __syncthreads();
     }
-    if (t == 0) {
-        counts[0] = carry;
+    int64_t run = part[t] - sum;
+    for (int64_t k = b; k < e; k++) {
+        const int64_t v = wave_cnt[k];
+        wave_cnt[k] = run;
+        run += v;
+    }
+    if (t == 1023) {
+        counts[0] = part[1023];
         counts[1] = 0;
-        seg_off[carry] = n;
+        seg_off[part[1023]] = n;
     }
 }
-// the segments of >= long_min updates, appended in any order
-__global__ __launch_bounds__(kSegBlock) void td_seg_long_kernel(const int64_t* __restrict__ seg_off,
-                                                                int64_t long_min, int64_t* __restrict__ long_idx,
-                                                                int64_t* __restrict__ counts) {
-    const int64_t n_seg = counts[0];
-    for (int64_t j = (int64_t)blockIdx.x * kSegBlock + threadIdx.x; j < n_seg; j += (int64_t)gridDim.x * kSegBlock) {
-        if (seg_off[j + 1] - seg_off[j] >= long_min) {
-            const int64_t at = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), 1ull);
-            long_idx[at] = j;
-        }
-    }
-}
-
 size_t split_bytes(int64_t n_old, int64_t n_upd, int64_t tile) {
     if (n_upd <= 0) return 0;
     return (size_t)((n_old + n_upd + tile - 1) / tile + 1) * sizeof(int64_t);
@@ -560,13 +556,13 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
     hipStream_t st = (hipStream_t)stream;
     int64_t* wave_cnt = static_cast<int64_t*>(temp);
     const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
-    if (n > 0) td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys);
+    if (n > 0)
+        td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys, long_min, long_idx,
+                                                          counts);
     td_seg_scan_kernel<<<1, 1024, 0, st>>>(wave_cnt, n_waves, n, seg_off, counts);
-    if (n > 0) {
-        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys);
-        const int64_t lb = std::min<int64_t>((n + kSegBlock - 1) / kSegBlock, 2048);
-        td_seg_long_kernel<<<(unsigned)lb, kSegBlock, 0, st>>>(seg_off, long_min, long_idx, counts);
-    }
+    if (n > 0)
+        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys, long_min, long_idx,
+                                                         counts);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OTH_OK : -(int)e;
 }

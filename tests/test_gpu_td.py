@@ -64,8 +64,8 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
     chunk starts, middles and ends of long segments and compare with the
     sequential rule in Python floats.  With long_min, oth_td_ema_split runs
     the segments at least that long on a whole wave each (LDS stages of 1024
-    values: lengths around multiples of the stage), those at least 4 warm-ups
-    long split into parts over a block's lanes (warm-up 64 at a = 0.5).  A
+    values: lengths around multiples of the stage), those at least 3 warm-ups
+    long split into parts over many waves (warm-up 86 at a = 0.5).  A
     warm-up of 1 or 3 values (OTH_TD_SPEC_WARM) makes most guesses miss: the
     rerun passes."""
     from subproc_amd import _lib
@@ -108,7 +108,7 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
 def test_td_ema_split_speculation_learner_rate(kind):
     """Long segments at the learner's rate (a = 0.03, warm-up 1,942 values: 4/3
     of the 2^-64 contraction length) split into parts of 1,040 (600,001 values:
-    577 parts over 10 one-wave work items; 7,767 values stay on one lane, 7,768
+    577 parts over 10 one-wave work items; 5,825 values stay on one lane, 5,826
     are split): the result is the sequential rule's, bit for bit,
     whether the lanes' guesses converge (random targets), sit on a fixed
     point of the rounding (a constant target) or run through exact zeros
@@ -117,7 +117,7 @@ def test_td_ema_split_speculation_learner_rate(kind):
     a = 0.03
     oma = 1 - a
     rng = np.random.default_rng({"normal": 5, "constant": 6, "sparse": 7}[kind])
-    lengths = [7767, 7768, 9000, 70001, 200003, 600001]
+    lengths = [5825, 5826, 9000, 70001, 200003, 600001]
     vals, seg, want = [], [0], []
     for L in lengths:
         if kind == "normal":

@@ -14,7 +14,7 @@ for v in build/var/spec*.so; do
   tail -4 $O/probe_$b.log
 done
 timeout -k 10 200 python3 tools/diag/td_trace.py 262144 4 2>&1 | tee $O/td_product.log
-for w in 1457; do
+for w in; do
   echo "== warm $w"
   OTH_TD_SPEC_WARM=$w timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr$w -o run -- python3 tools/diag/td_spec_probe.py > $O/probe_w$w.log 2>&1 || { tail -5 $O/probe_w$w.log; exit 1; }
   grep -v "^W2026\|^E2026" $O/probe_w$w.log | tail -4

@@ -339,7 +339,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
  * by): counts[0] = n_seg, the number of distinct keys; seg_off[0..n_seg] the
  * offsets of their runs (seg_off[j] = first index of key j, seg_off[n_seg]
  * = n); ukeys[0..n_seg) the keys; long_idx[0..counts[1]) the indices j of
- * the segments of >= long_min updates, in no particular order (what
+ * the segments of >= long_min updates, in increasing order (what
  * oth_td_ema_split takes).  seg_off holds n + 1 entries, ukeys and long_idx
  * n (capacities: the counts are known only after the call); counts (2
  * int64) is device memory, like the rest.  temp / temp_bytes as

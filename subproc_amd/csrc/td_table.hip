@@ -21,6 +21,7 @@
 
 #include <climits>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "../../include/othello.h"
 
@@ -344,55 +345,74 @@ hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t 
 // segment starts where a key differs from the one before (the lane's
 // neighbour by a DPP shift, the round's first from the round before), a
 // ballot and mbcnt place the starts.  A count pass and a write pass around a
-// scan of the waves' counts keep the order; the long segments are listed by
-// atomic appends, in no particular order (their consumers take any order).
+// scan of the waves' counts (rocPRIM) keep the order; the long segments the
+// same way, by a second ballot and scan.
 constexpr int kSegRounds = 16;
 constexpr int kSegWaveKeys = 64 * kSegRounds;
 constexpr int kSegBlock = 256;
 constexpr int kSegWavesPerBlock = kSegBlock / 64;
-// WRITE: a segment that starts at i is long iff keys[i + long_min - 1] is
-// its key (the keys are sorted): one more load per start, mostly from the
-// same lines, and an atomic append; no pass of its own over the offsets
+// A segment that starts at i is long iff keys[i + long_min - 1] is its key
+// (the keys are sorted), read from the wave's keys staged in LDS (with the
+// next round's).  Both passes find starts and long starts; the count pass
+// leaves the wave's two counts, the write pass (after their scans) places
+// both in order.  (The long keys by atomic appends instead: 25k appends to
+// one counter cost the write pass 83 -> 368 us.)
 template <bool WRITE>
 __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __restrict__ keys, int64_t n,
                                                            int64_t* __restrict__ wave_cnt,
+                                                           int64_t* __restrict__ wave_lcnt,
                                                            int64_t* __restrict__ seg_off,
                                                            int64_t* __restrict__ ukeys, int64_t long_min,
-                                                           int64_t* __restrict__ long_idx,
-                                                           int64_t* __restrict__ counts) {
+                                                           int64_t* __restrict__ long_idx) {
+    __shared__ int64_t stage[kSegWavesPerBlock][kSegWaveKeys + 64];
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
     const int64_t base = w * kSegWaveKeys;
     if (base >= n) return;  // wave-uniform
-    // every round's key loaded before the first is used (16 loads in flight)
+    // every round's key loaded before the first is used (17 loads in flight)
     int64_t k[kSegRounds];
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
         k[r] = i < n ? keys[i] : 0;
     }
+    int64_t* mine = stage[threadIdx.x >> 6];
+    {
+        const int64_t i = base + kSegWaveKeys + lane;
+        mine[kSegWaveKeys + lane] = i < n ? keys[i] : -1;  // (keys are >= 0)
+    }
+#pragma unroll
+    for (int r = 0; r < kSegRounds; r++) mine[r * 64 + lane] = k[r];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     int64_t prev_last = base > 0 ? keys[base - 1] : 0;
-    int64_t pos = WRITE ? wave_cnt[w] : 0;  // the wave's first segment index (after the scan)
+    int64_t pos = WRITE ? wave_cnt[w] : 0, lpos = WRITE ? wave_lcnt[w] : 0;  // after the scans: the wave's firsts
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
         const bool start = i < n && (i == 0 || k[r] != before);
-        const uint64_t m = __ballot(start);
+        const int64_t e = i + long_min - 1, off = e - base;
+        const bool lng = start && e < n && (off < kSegWaveKeys + 64 ? mine[off] == k[r] : keys[e] == k[r]);
+        const uint64_t m = __ballot(start), ml = __ballot(lng);
         if (WRITE && start) {
             const int64_t at =
                 pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             seg_off[at] = i;
             ukeys[at] = k[r];
-            const int64_t e = i + long_min - 1;
-            if (e < n && keys[e] == k[r])
-                long_idx[atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), 1ull)] = at;
+            if (lng)
+                long_idx[lpos + __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u))] = at;
         }
         pos += __popcll(m);
+        lpos += __popcll(ml);
         prev_last = __shfl(k[r], 63);
     }
-    if (!WRITE && lane == 0) wave_cnt[w] = pos;
+    if (!WRITE && lane == 0) {
+        wave_cnt[w] = pos;
+        wave_lcnt[w] = lpos;
+    }
 }
 // the exclusive running count of is_new (oth_td_new_before), the same two
 // passes: per wave a count, then, after the scan, every position's count
@@ -416,39 +436,35 @@ __global__ __launch_bounds__(kSegBlock) void td_count_kernel(const uint8_t* __re
     }
     if (!WRITE && lane == 0) wave_cnt[w] = pos;
 }
-// one block: exclusive scan of the waves' counts in place, the total into
-// counts[0], seg_off[total] = n, counts[1] (the long segments' counter) = 0
-// (thread t owns the run [t * per, (t + 1) * per) of the counts: its serial
-// sum, a block scan of the 1,024 sums, then its run's prefixes)
-__global__ __launch_bounds__(1024) void td_seg_scan_kernel(int64_t* __restrict__ wave_cnt, int64_t n_waves, int64_t n,
-                                                           int64_t* __restrict__ seg_off,
-                                                           int64_t* __restrict__ counts) {
-    __shared__ int64_t part[1024];
-    const int t = threadIdx.x;
-    const int64_t per = (n_waves + 1023) / 1024;
-    const int64_t b = min<int64_t>(t * per, n_waves), e = min<int64_t>(b + per, n_waves);
-    int64_t sum = 0;
-    for (int64_t k = b; k < e; k++) sum += wave_cnt[k];
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the 1,024 sums
-        const int64_t add = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += add;
-        __syncthreads();
-    }
-    int64_t run = part[t] - sum;
-    for (int64_t k = b; k < e; k++) {
-        const int64_t v = wave_cnt[k];
-        wave_cnt[k] = run;
-        run += v;
-    }
-    if (t == 1023) {
-        counts[0] = part[1023];
-        counts[1] = 0;
-        seg_off[part[1023]] = n;
-    }
+// after the exclusive scan of the waves' counts (wave_off): the total into
+// *total, and end_slot_base[total] = n (if given)
+__global__ void td_seg_finish_kernel(const int64_t* __restrict__ wave_cnt, const int64_t* __restrict__ wave_off,
+                                     int64_t n_waves, int64_t n, int64_t* __restrict__ end_slot_base,
+                                     int64_t* __restrict__ total_out) {
+    const int64_t total = n_waves > 0 ? wave_off[n_waves - 1] + wave_cnt[n_waves - 1] : 0;
+    *total_out = total;
+    if (end_slot_base) end_slot_base[total] = n;
 }
+// the waves' counts -> their exclusive prefixes (rocPRIM's device scan), then
+// the finish kernel; temp: [wave_cnt | wave_off | rocPRIM's scratch]
+hipError_t seg_scan(int64_t* wave_cnt, int64_t* wave_off, int64_t n_waves, int64_t n, int64_t* end_slot_base,
+                    int64_t* total_out, void* scan_temp, size_t scan_bytes, hipStream_t st) {
+    if (n_waves > 0) {
+        const hipError_t e = rocprim::exclusive_scan(scan_temp, scan_bytes, wave_cnt, wave_off, (int64_t)0,
+                                                     (size_t)n_waves, rocprim::plus<int64_t>(), st);
+        if (e != hipSuccess) return e;
+    }
+    td_seg_finish_kernel<<<1, 1, 0, st>>>(wave_cnt, wave_off, n_waves, n, end_slot_base, total_out);
+    return hipGetLastError();
+}
+size_t seg_scan_bytes(int64_t n_waves) {
+    size_t b = 0;
+    const int64_t* nul = nullptr;
+    (void)rocprim::exclusive_scan(nullptr, b, nul, (int64_t*)nullptr, (int64_t)0, (size_t)(n_waves > 0 ? n_waves : 1),
+                                  rocprim::plus<int64_t>());
+    return b;
+}
+
 size_t split_bytes(int64_t n_old, int64_t n_upd, int64_t tile) {
     if (n_upd <= 0) return 0;
     return (size_t)((n_old + n_upd + tile - 1) / tile + 1) * sizeof(int64_t);
@@ -546,8 +562,10 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
                     int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream) {
     if (n < 0 || long_min < 1 || !temp_bytes) return OTH_EINVAL;
-    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys;
-    const size_t need = (size_t)(n_waves > 0 ? n_waves : 1) * sizeof(int64_t);
+    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys, slots = n_waves > 0 ? n_waves : 1;
+    const size_t scan_bytes = seg_scan_bytes(n_waves);
+    const size_t head = (4 * (size_t)slots * sizeof(int64_t) + 255) / 256 * 256;  // rocPRIM's scratch 256-B aligned
+    const size_t need = head + scan_bytes;
     if (!temp) {  // size query: no work, no launch
         *temp_bytes = need;
         return OTH_OK;
@@ -555,23 +573,31 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
     if (!seg_off || !counts || (n > 0 && (!keys || !ukeys || !long_idx)) || *temp_bytes < need) return OTH_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     int64_t* wave_cnt = static_cast<int64_t*>(temp);
+    int64_t* wave_off = wave_cnt + slots;
+    int64_t* wave_lcnt = wave_off + slots;
+    int64_t* wave_loff = wave_lcnt + slots;
+    void* scan_temp = static_cast<char*>(temp) + head;
     const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
     if (n > 0)
-        td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys, long_min, long_idx,
-                                                          counts);
-    td_seg_scan_kernel<<<1, 1024, 0, st>>>(wave_cnt, n_waves, n, seg_off, counts);
+        td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, wave_lcnt, seg_off, ukeys, long_min,
+                                                          long_idx);
+    hipError_t e = seg_scan(wave_cnt, wave_off, n_waves, n, seg_off, counts, scan_temp, scan_bytes, st);
+    if (e == hipSuccess) e = seg_scan(wave_lcnt, wave_loff, n_waves, n, nullptr, counts + 1, scan_temp, scan_bytes, st);
+    if (e != hipSuccess) return -(int)e;
     if (n > 0)
-        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, seg_off, ukeys, long_min, long_idx,
-                                                         counts);
-    const hipError_t e = hipGetLastError();
+        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_off, wave_loff, seg_off, ukeys, long_min,
+                                                         long_idx);
+    e = hipGetLastError();
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 
 int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
                       void* stream) {
     if (n < 0 || !temp_bytes) return OTH_EINVAL;
-    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys;
-    const size_t need = (size_t)(n_waves > 0 ? n_waves : 1) * sizeof(int64_t) + 2 * sizeof(int64_t);
+    const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys, slots = n_waves > 0 ? n_waves : 1;
+    const size_t scan_bytes = seg_scan_bytes(n_waves);
+    const size_t head = (2 * (size_t)slots * sizeof(int64_t) + 2 * sizeof(int64_t) + 255) / 256 * 256;
+    const size_t need = head + scan_bytes;
     if (!temp) {  // size query: no work, no launch
         *temp_bytes = need;
         return OTH_OK;
@@ -579,14 +605,15 @@ int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, voi
     if (!new_before || (n > 0 && !is_new) || *temp_bytes < need) return OTH_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     int64_t* wave_cnt = static_cast<int64_t*>(temp);
-    int64_t* counts = wave_cnt + (n_waves > 0 ? n_waves : 1);  // the scan kernel's [total, 0]
+    int64_t* wave_off = wave_cnt + slots;
+    int64_t* counts = wave_off + slots;  // [total, unused]
     const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
     if (n > 0) td_count_kernel<false><<<blocks, kSegBlock, 0, st>>>(is_new, n, wave_cnt, new_before);
-    // (the scan writes new_before[total] = n first; the write pass below and
-    // the copy of the total into new_before[n] then overwrite what they own)
-    td_seg_scan_kernel<<<1, 1024, 0, st>>>(wave_cnt, n_waves, n, new_before, counts);
-    if (n > 0) td_count_kernel<true><<<blocks, kSegBlock, 0, st>>>(is_new, n, wave_cnt, new_before);
-    hipError_t e = hipGetLastError();
+    hipError_t e = seg_scan(wave_cnt, wave_off, n_waves, n, nullptr, counts, static_cast<char*>(temp) + head,
+                            scan_bytes, st);  // counts[0] = the total
+    if (e != hipSuccess) return -(int)e;
+    if (n > 0) td_count_kernel<true><<<blocks, kSegBlock, 0, st>>>(is_new, n, wave_off, new_before);
+    e = hipGetLastError();
     if (e == hipSuccess)
         e = hipMemcpyAsync(new_before + n, counts, sizeof(int64_t), hipMemcpyDeviceToDevice, st);
     return e == hipSuccess ? OTH_OK : -(int)e;

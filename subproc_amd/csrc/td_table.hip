@@ -59,7 +59,13 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
 }
 
 constexpr int kMergeBlock = 256;
-constexpr int kMergeK = 8;                               // merged positions per thread
+#ifndef OTH_MERGE_K  // A/B builds only
+#define OTH_MERGE_K 8
+#endif
+#ifndef OTH_MERGE_DEFER  // A/B builds only
+#define OTH_MERGE_DEFER 1
+#endif
+constexpr int kMergeK = OTH_MERGE_K;                     // merged positions per thread
 constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
 constexpr int kLookupK = 8;
 constexpr int kLookupTile = kMergeBlock * kLookupK;
@@ -146,6 +152,46 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     double ov[kMergeK];
     uint64_t os[kMergeK];
     unsigned long long smin = ~0ull, smax = 0;
+#if OTH_MERGE_DEFER
+    // the merge walk first, recording each output's batch index; then the
+    // new_before loads of all of them at once (in the walk they were one
+    // dependent global load per step; round 4)
+    int64_t bq[kMergeK];
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) {
+        bq[q] = -1;  // no output
+        const int m = t0 + q;
+        if (m >= t1) continue;
+        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
+            const int64_t key = sk[i];
+            if (key != prev_b) {  // not the table copy of the batch key just taken
+                bq[q] = b0 + j;
+                ok[q] = key;
+                ov[q] = sv[i];
+            }
+            i++;
+        } else {
+            const int64_t key = sk[na + j];
+            bq[q] = b0 + j;
+            ok[q] = key;
+            ov[q] = sv[na + j];
+            prev_b = key;
+            j++;
+        }
+    }
+    int64_t nbq[kMergeK];
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) nbq[q] = bq[q] >= 0 ? new_before[bq[q]] : 0;
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) {
+        os[q] = bq[q] >= 0 ? (uint64_t)(d0 + t0 + q - (bq[q] - nbq[q])) : ~0ull;
+        if (os[q] >= n_out) os[q] = ~0ull;
+        if (os[q] != ~0ull) {
+            smin = min(smin, (unsigned long long)os[q]);
+            smax = max(smax, (unsigned long long)os[q] + 1);
+        }
+    }
+#else
 #pragma unroll
     for (int q = 0; q < kMergeK; q++) {
         os[q] = ~0ull;  // no output
@@ -176,6 +222,7 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
             smax = max(smax, (unsigned long long)os[q] + 1);
         }
     }
+#endif
     if (smin != ~0ull) {
         atomicMin(&range[0], smin);
         atomicMax(&range[1], smax);

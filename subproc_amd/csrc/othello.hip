@@ -184,7 +184,7 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
-#ifndef OTH_COOP_HOLD_EVAL  // A/B builds only (tools/gpu_ab.sh)
+#ifndef OTH_COOP_HOLD_EVAL  // A/B builds only (held, the eval kernel spills)
 #define OTH_COOP_HOLD_EVAL 0
 #endif
 struct CoopWave {

@@ -27,8 +27,8 @@
 
 namespace {
 
-// onesweep digit width and items per thread (build knobs for A/B builds only:
-// tools/gpu_ab.sh; the product build uses the defaults)
+// onesweep digit width, items per thread and block size (build knobs for A/B
+// builds only; the product build uses the defaults)
 #ifndef OTH_SORT_BITS
 #define OTH_SORT_BITS 9
 #endif

@@ -15,7 +15,7 @@ from subproc_amd.td import StateMap  # noqa: E402
 
 args = [x for x in sys.argv[1:] if not x.startswith("--lib=")]
 for x in sys.argv[1:]:
-    if x.startswith("--lib="):  # an A/B build of the whole library (tools/gpu_ab.sh)
+    if x.startswith("--lib="):  # an A/B build of the whole library (tools/gpu_merge_ab.sh)
         from subproc_amd import _lib
         _lib.LIB_PATH = os.path.abspath(x[len("--lib="):])
 games = int(args[0]) if len(args) > 0 else 1 << 18

@@ -230,6 +230,13 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 // bit-reversed board.  Table rows: 0..2 = rays +8, +9, +7 (normal order),
 // 3..5 = rays -8, -9, -7 stored bit-reversed; 64 squares each (3 KiB).
 constexpr int kRayRows = 6;
+// OTH_FLIPS_NORMAL_DEC (A/B builds only, round 4): the three decreasing rays'
+// flips in normal orientation, by the ray's highest non-run square (v_ffbh),
+// instead of on the bit-reversed board; table rows 3..5 then hold the rays
+// in normal orientation and the run sets keep A2 / A4 / A6 unreversed
+#ifndef OTH_FLIPS_NORMAL_DEC
+#define OTH_FLIPS_NORMAL_DEC 0
+#endif
 // the LDS table adds two rows per square: 6 = the square's bit, 7 = its bit
 // on the reversed board (1 << (63 - sq)); read with the rays, they replace two
 // variable 64-bit shifts of the VALU-bound loop by LDS reads
@@ -254,7 +261,7 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
             continue;
         }
         const u64 r = ray_from(sq, dx[row], dy[row]);
-        tab[e] = row < 3 ? r : rev64(r);
+        tab[e] = (row < 3 || OTH_FLIPS_NORMAL_DEC) ? r : rev64(r);
     }
 }
 // the move's bit from the table (row kRayRows)
@@ -279,7 +286,21 @@ struct RunSets {
     u64 A1, A3, A5, A7, rA0, rA2, rA4, rA6;
 };
 __device__ __forceinline__ RunSets run_sets(const Position& s) {
+#if OTH_FLIPS_NORMAL_DEC
+    return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), s.A[2], s.A[4], s.A[6]};
+#else
     return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), rev64(s.A[2]), rev64(s.A[4]), rev64(s.A[6])};
+#endif
+}
+// For a ray R leaving the move in decreasing bit order (normal orientation)
+// and the run set A: the squares of R & A above R's highest square not in A
+// (x = R & ~A, nonzero whenever R & A is)
+__device__ __forceinline__ u64 run_prefix_dec(u64 R, u64 A) {
+    const u64 x = andn(R, A);
+    const u32 hi = (u32)(x >> 32), lo = (u32)x;
+    const u32 top = hi ? 63u - (u32)__builtin_clz(hi) : 31u - (u32)__builtin_clz(lo | 1u);
+    const u64 below = dec64(2ull << top);  // bits 0..top (2 << 63 wraps to 0: all)
+    return bitop3<0x20>(R, below, A);       // R & ~below & A
 }
 
 // The flips of the move at square sq (bit mv) in two parts, both including
@@ -304,8 +325,13 @@ __device__ __forceinline__ Flips flips_col(u64 mv, const RunSets& r, const u64* 
     u64 fr = bitop3<0xBA>(r.rA0, lshl1_add(rmv, r.rA0), rmv);  // west, in reversed space
     f = or3(f, run_prefix(col[0 * 64], r.A3), run_prefix(col[1 * 64], r.A5));
     f = or2(f, run_prefix(col[2 * 64], r.A7));
+#if OTH_FLIPS_NORMAL_DEC
+    f = or3(f, run_prefix_dec(col[3 * 64], r.rA2), run_prefix_dec(col[4 * 64], r.rA4));
+    f = or2(f, run_prefix_dec(col[5 * 64], r.rA6));
+#else
     fr = or3(fr, run_prefix(col[3 * 64], r.rA2), run_prefix(col[4 * 64], r.rA4));
     fr = or2(fr, run_prefix(col[5 * 64], r.rA6));
+#endif
     return Flips{f, rev64(fr)};
 }
 __device__ __forceinline__ Flips flips_rays(u32 sq, const RunSets& r, const u64* tab) {

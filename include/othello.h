@@ -307,7 +307,9 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
  * missed.  long_idx (device, n_long entries) must list every segment of
  * length >= long_min, in any order, each once; a segment that long missing
  * from it is left unwritten.  n_values = seg_off[n_seg], the length of
- * values.  temp / temp_bytes: device scratch of the split (its plan, the
+ * values; it sizes the split's scratch, and a smaller n_values only makes
+ * the keys whose parts do not fit run unsplit (sequentially, same result;
+ * nothing is written past the scratch).  temp / temp_bytes: device scratch of the split (its plan, the
  * parts' guesses and end states), the caller's; temp == NULL is a size query
  * (*temp_bytes receives the size for these n_long and n_values, nothing else
  * happens), otherwise *temp_bytes is the size of temp.  Same results as
@@ -320,7 +322,8 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
  * of oth_td_updates / oth_td_updates_rows (row_off NULL: the strided table)
  * with each update as one uint64 word,
  *   (value_side + 64) << 56 | turn_left << 43 | OTH_TD_KEY,
- * turn_left = plies[g] - p (0..128), value_side = +-(n_black - n_white) of
+ * turn_left = min(plies[g], OTH_MOVES_STRIDE) - p (0..128; the clamp
+ * oth_td_updates applies too), value_side = +-(n_black - n_white) of
  * the terminal: the value is value_side * lam_pow[turn_left], exactly the
  * double oth_td_updates writes, and oth_td_unpack recomputes it.  Half the
  * bytes of a (key, value) pair, and the grouping sort becomes a keys-only

@@ -1155,17 +1155,20 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
     // the block's rows of pos_turn / pos_end are one contiguous range each:
     // global bytes [base, base + bytes), staged from base_al
     // the game of a staged byte (the escape path only): by division, or by a
-    // search of the block's row offsets
+    // linear scan of the block's games for the one whose rows
+    // [row_off, row_off + plies] hold it.  The offsets of a staged block need
+    // not increase (any disjoint layout stages), so no binary search; an
+    // escaped byte is rare (a start turn >= 127 still to move) and a block has
+    // at most 256 games.  Escape bytes are only ever staged for a game's own
+    // rows, so the scan always finds one.
     auto game_of = [&](int64_t q) -> int64_t {
         if (!PACKED) return blk0 + q / OTH_POS_STRIDE;
         const int64_t row = base_al + q;
-        int lo = 0, hi = nb - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (row_off[blk0 + mid] <= row) lo = mid;
-            else hi = mid - 1;
+        for (int k = 0; k < nb; k++) {
+            const int64_t r0 = row_off[blk0 + k];
+            if (row >= r0 && row <= r0 + min<int>(plies[blk0 + k], OTH_MOVES_STRIDE)) return blk0 + k;
         }
-        return blk0 + lo;
+        return blk0;
     };
     if (vec_out) {
         for (int c = lane; c * 16 < span; c += kBlock) {
@@ -1701,36 +1704,40 @@ __global__ __launch_bounds__(kBlock) void td_spec_select_kernel(const int64_t* _
     plan[slot] = SpecPlanEntry{s, 0, 0, spec_parts(n)};
 }
 // one block: the running offsets of the selected keys' parts and work items
-// (exclusive scans over the plan), and the totals into hdr[0..2]
+// (exclusive scans over the plan), and the totals into hdr[0..2].  cap: the
+// parts the scratch holds (the caller's n_values sizes it).  A key whose parts
+// would end past cap (n_values below seg_off[n_seg], a caller error the
+// header names) gets no parts and no work items: td_spec_fix_kernel then runs
+// it sequentially, so no part is ever written out of bounds.
 __global__ __launch_bounds__(1024) void td_spec_plan_kernel(int64_t* __restrict__ hdr,
-                                                            SpecPlanEntry* __restrict__ plan) {
+                                                            SpecPlanEntry* __restrict__ plan, int64_t cap) {
     __shared__ u32 wsum[2][16];
     __shared__ int64_t carry[2];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t n_spec = hdr[3];
     if (t < 2) carry[t] = 0;
     __syncthreads();
+    // an inclusive block scan of x (channel c): returns the exclusive prefix
+    // over the keys before this one, the carry of earlier rounds included
+    auto block_excl = [&](u32 x, int c) -> int64_t {
+        const u32 incl = wave_incl_scan(x);
+        if (lane == 63) wsum[c][wv] = incl;
+        __syncthreads();
+        u32 before = 0;
+        for (int w2 = 0; w2 < wv; w2++) before += wsum[c][w2];
+        return carry[c] + before + incl - x;
+    };
     for (int64_t t0 = 0; t0 < n_spec; t0 += 1024) {
         const int64_t k = t0 + t;
-        const u32 P = k < n_spec ? (u32)plan[k].n_parts : 0u, C = (P + kSpecLanes - 1) / kSpecLanes;
-        const u32 in[2] = {P, C};
-        u32 incl[2];
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            incl[c] = wave_incl_scan(in[c]);
-            if (lane == 63) wsum[c][wv] = incl[c];
-        }
-        __syncthreads();
-        int64_t ex[2];
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            u32 before = 0;
-            for (int w2 = 0; w2 < wv; w2++) before += wsum[c][w2];
-            ex[c] = carry[c] + before + incl[c] - in[c];
-        }
+        u32 P = k < n_spec ? (u32)plan[k].n_parts : 0u;
+        const int64_t pbase = block_excl(P, 0);
+        if (pbase + P > cap) P = 0;  // does not fit: sequential in td_spec_fix_kernel
+        const u32 C = (P + kSpecLanes - 1) / kSpecLanes;
+        const int64_t ibase = block_excl(C, 1);
         if (k < n_spec) {
-            plan[k].part_base = ex[0];
-            plan[k].item_base = ex[1];
+            plan[k].n_parts = P;
+            plan[k].part_base = pbase;
+            plan[k].item_base = ibase;
         }
         __syncthreads();
         if (t < 2) {
@@ -1786,7 +1793,8 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double*
 // one wave per split key: its parts checked in order, 64 at a time; missed
 // guesses rerun from their predecessor's end state until all match
 __global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* __restrict__ vals,
-                                                                 const int64_t* __restrict__ seg_off, double a,
+                                                                 const int64_t* __restrict__ seg_off,
+                                                                 const double* __restrict__ init, double a,
                                                                  double oma, const int64_t* __restrict__ hdr,
                                                                  const SpecPlanEntry* __restrict__ plan,
                                                                  const double* __restrict__ guess,
@@ -1800,6 +1808,12 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* _
         const int64_t np = uniform64(plan[key].n_parts);
         const int64_t b = uniform64(seg_off[s]);
         const int n = (int)uniform64(seg_off[s + 1] - b);
+        if (np == 0) {  // parts past the scratch (td_spec_plan_kernel): the whole key on lane 0
+            double v = init ? init[s] : 0.0, unused = v;
+            spec_stream(vals + b, n, lane == 0, 0, 0, n, v, unused, a, oma, sh);
+            if (lane == 0) out[s] = v;
+            continue;
+        }
         double prev = 0.0;  // the end state of the part before this chunk's first
         for (int64_t c0 = 0; c0 < np; c0 += kSpecLanes) {
             const int64_t q = c0 + lane;
@@ -2324,7 +2338,7 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
                                                                                     kSpecMinWarms * warm, hdr, plan);
     rc = launched();
     if (rc != OTH_OK) return rc;
-    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan);
+    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan, parts);
     rc = launched();
     if (rc != OTH_OK) return rc;
     const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
@@ -2334,7 +2348,7 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     rc = launched();
     if (rc != OTH_OK) return rc;
     td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, (hipStream_t)stream>>>(
-        values, seg_off, a, one_minus_a, hdr, plan, guess, fin, out);
+        values, seg_off, init, a, one_minus_a, hdr, plan, guess, fin, out);
     return launched();
 }
 

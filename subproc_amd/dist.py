@@ -56,12 +56,21 @@ def rollout_sharded(total_games, seed, policy="random", n_random=10, group=None,
         if rollout_fn is None:
             from . import ops
             per, rest = divmod(local, steps)
-            if per:  # `steps` equal launches, then the remainder
-                ops.rollout_batches(per, steps, seed, game_id_base + begin, policy, n_random, hist=hist, device=device,
-                                    streams=streams)
-            if rest:
-                ops.rollout(rest, seed, game_id_base + begin + per * steps, policy, n_random, hist=hist,
-                            device=device, want_boards=False, want_diff=False, want_plies=False)
+            if steps == 1 or streams == 1:
+                # one launch per chunk on the caller's stream (no side stream,
+                # no fork/join events: capturable, as before round 4)
+                for c in range(steps):
+                    b, e = shard_range(local, c, steps)
+                    if e > b:
+                        ops.rollout(e - b, seed, game_id_base + begin + b, policy, n_random, hist=hist,
+                                    device=device, want_boards=False, want_diff=False, want_plies=False)
+            else:
+                if per:  # `steps` equal launches, then the remainder
+                    ops.rollout_batches(per, steps, seed, game_id_base + begin, policy, n_random, hist=hist,
+                                        device=device, streams=streams)
+                if rest:
+                    ops.rollout(rest, seed, game_id_base + begin + per * steps, policy, n_random, hist=hist,
+                                device=device, want_boards=False, want_diff=False, want_plies=False)
         else:
             for c in range(steps):
                 b, e = shard_range(local, c, steps)

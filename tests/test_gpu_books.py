@@ -240,3 +240,41 @@ def test_replay_rows_non_monotonic_offsets():
             assert torch.equal(b[rows], full.boards[inside])
             tt, ee = t[shift:shift + total], e[shift:shift + total]
             assert torch.equal(tt[rows], full.turn[inside]) and torch.equal(ee[rows], full.end[inside])
+
+
+def test_replay_rows_non_monotonic_offsets_escaped_turns():
+    """Offsets shuffled inside each 256-game block (staged) with start turns
+    0, 1, 2, 200 and a pass first, so escaped turn bytes (start turn >= 127)
+    sit in blocks whose offsets do not increase: the escape's
+    game is found by a scan of the block's rows, not a binary search."""
+    from subproc_amd import _lib
+    n = 1500
+    rng = np.random.default_rng(21)
+    r = ops.rollout(n, 13, 5, record_moves=True, device="cuda")
+    start = r.final_boards.clone()
+    stt = torch.as_tensor(rng.choice([0, 1, 2, 200], n).astype(np.uint8)).cuda()
+    mv = torch.as_tensor(rng.integers(0, 66, (n, 128)).astype(np.uint8)).cuda()
+    mv[:, 0] = 64  # a pass first: row 0 holds the start turn (escaped when 200), then put_s turns
+    pl = torch.as_tensor(rng.integers(0, 40, n).astype(np.uint8)).cuda()
+    full = ops.replay(mv, pl, start, stt)
+    inside = torch.arange(129, device="cuda")[None, :] <= pl.long()[:, None]
+    cnt = (pl.long() + 1).cpu().numpy()
+    within = np.concatenate([rng.permutation(np.arange(b, min(b + 256, n))) for b in range(0, n, 256)])
+    L = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    total = int(cnt.sum())
+    for order in (np.arange(n)[::-1], within):
+        off_np = np.zeros(n, np.int64)
+        off_np[order] = np.cumsum(cnt[order]) - cnt[order]
+        off = torch.as_tensor(off_np).cuda()
+        for shift in (0, 1):
+            b = torch.full((total, 2), 7, dtype=torch.int64, device="cuda")
+            t = torch.full((total + 1,), 0xAB, dtype=torch.uint8, device="cuda")
+            e = torch.full((total + 1,), 0xCD, dtype=torch.uint8, device="cuda")
+            assert L.oth_replay_rows(start.data_ptr(), stt.data_ptr(), mv.data_ptr(), pl.data_ptr(), off.data_ptr(),
+                                     b.data_ptr(), t.data_ptr() + shift, e.data_ptr() + shift, n, s) == 0
+            rows = (off[:, None] + torch.arange(129, device="cuda")[None, :])[inside]
+            assert torch.equal(b[rows], full.boards[inside])
+            tt, ee = t[shift:shift + total], e[shift:shift + total]
+            assert int((full.turn[inside] == 200).sum()) > 100  # escapes are exercised
+            assert torch.equal(tt[rows], full.turn[inside]) and torch.equal(ee[rows], full.end[inside])

@@ -104,15 +104,17 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
     assert out.cpu().tolist() == [w[1] for w in want]
 
 
-@pytest.mark.parametrize("kind", ["normal", "constant", "sparse"])
-def test_td_ema_split_speculation_learner_rate(kind):
+@pytest.mark.parametrize("kind,short", [("normal", False), ("constant", False), ("sparse", False), ("normal", True)])
+def test_td_ema_split_speculation_learner_rate(kind, short):
     """Long segments at the learner's rate (a = 0.03, warm-up 1,942 values: 4/3
     of the 2^-64 contraction length) split into parts of 1,040 (600,001 values:
     577 parts over 10 one-wave work items; 5,825 values stay on one lane, 5,826
     are split): the result is the sequential rule's, bit for bit,
     whether the lanes' guesses converge (random targets), sit on a fixed
     point of the rounding (a constant target) or run through exact zeros
-    (mostly-zero targets: draws)."""
+    (mostly-zero targets: draws).  short: n_values far below seg_off[n_seg]
+    (ADVICE r4), so the scratch holds the parts of the first keys only; the
+    keys that do not fit run unsplit, same results, nothing written past it."""
     from subproc_amd import _lib
     a = 0.03
     oma = 1 - a
@@ -139,7 +141,8 @@ def test_td_ema_split_speculation_learner_rate(kind):
     li = torch.arange(len(lengths), dtype=torch.int64, device=DEV)
     lib = _lib.load()
     td._with_scratch(lib.oth_td_ema_split, (dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma, out.data_ptr(),
-                                            len(lengths), 1024, li.data_ptr(), li.numel(), dv.numel()),
+                                            len(lengths), 1024, li.data_ptr(), li.numel(),
+                                            10_000 if short else dv.numel()),
                      torch.cuda.current_stream().cuda_stream, DEV, "oth_td_ema_split")
     assert out.cpu().tolist() == want
 

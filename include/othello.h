@@ -334,10 +334,18 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream);
 /* Stable sort of n packed words by bits 0..OTH_TD_KEY_BITS-1 (the key):
- * equal keys keep their stream order.  temp / temp_bytes as
- * oth_td_sort_pairs. */
+ * equal keys keep their stream order; words_out distinct from words_in.
+ * temp / temp_bytes as oth_td_sort_pairs.  (The build's own LSD radix sort,
+ * round 5; round 4 called rocPRIM's.) */
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream);
+/* oth_td_sort_packed followed by oth_td_unpack in one: the sorted words'
+ * keys and values (keys[i] = the i-th sorted word's low OTH_TD_KEY_BITS,
+ * values[i] = value_side * lam_pow[turn_left]), the last radix pass writing
+ * them directly.  keys distinct from words_in.  temp / temp_bytes as
+ * oth_td_sort_pairs (round 5). */
+int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t* keys, double* values, int64_t n,
+                       void* temp, size_t* temp_bytes, void* stream);
 /* The segments of a key-sorted update stream (what StateMap.update groups
  * by): counts[0] = n_seg, the number of distinct keys; seg_off[0..n_seg] the
  * offsets of their runs (seg_off[j] = first index of key j, seg_off[n_seg]

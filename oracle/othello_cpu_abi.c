@@ -459,6 +459,26 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     return OTH_OK;
 }
 
+/* the sort, then the unpack of the sorted words (temp: the sort's scratch
+ * plus the sorted words) */
+int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t* keys, double* values, int64_t n,
+                       void* temp, size_t* temp_bytes, void* stream) {
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+    size_t sort_bytes = 0;
+    oth_td_sort_packed(NULL, NULL, n, NULL, &sort_bytes, stream);
+    const size_t need = sort_bytes + (size_t)(n > 0 ? n : 1) * sizeof(uint64_t);
+    if (!temp) {
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (*temp_bytes < need || (n > 0 && (!words_in || !lam_pow || !keys || !values || (const void*)words_in == (const void*)keys)))
+        return OTH_EINVAL;
+    uint64_t* sorted = (uint64_t*)((char*)temp + sort_bytes);
+    int rc = oth_td_sort_packed(words_in, sorted, n, temp, &sort_bytes, stream);
+    if (rc != OTH_OK) return rc;
+    return oth_td_unpack(sorted, lam_pow, keys, values, n, stream);
+}
+
 /* the regression sums in one row (the other rows zero): same contract */
 int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, const double* mean, double* partials,
                        void* stream) {

@@ -57,6 +57,7 @@ SIGNATURES = {
     "oth_rollout_grid": (_I, [_I, _I64]),
     "oth_td_updates_packed": (_I, [_P, _P, _P, _P, _P, _I64, _P]),
     "oth_td_sort_packed": (_I, [_P, _P, _I64, _P, _P, _P]),
+    "oth_td_sort_unpack": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),
     "oth_td_unpack": (_I, [_P, _P, _P, _P, _I64, _P]),
     "oth_td_merge": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),

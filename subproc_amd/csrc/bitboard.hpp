@@ -350,45 +350,64 @@ __device__ __forceinline__ const u64* ray_col(const u64* tab, u32 off) {
 // ---------------------------------------------------------------------------
 // Flips of one move without run sets (the single-step kernel, where the mover's
 // analysis is not otherwise needed).  Along a ray R leaving the move in
-// increasing bit order, the carry of (O | ~R) + (first square of R) ripples
-// through the opponent discs at the start of the ray and the non-ray bits
-// between them, and stops on the first ray square that is not an opponent
-// disc, which it sets.  The opponent squares it cleared are the run; they flip
-// iff the stop square holds a P disc.  A run that reaches the edge carries out
-// of the ray: no stop square, no flips.  An off-board ray is empty, so nothing
-// is selected from it.
-__device__ __forceinline__ u64 ray_flips(u64 first, u64 R, u64 P, u64 O) {
-    const u64 sum = add64(bfi(R, O, ~0ull), first);  // (O | ~R) + first
-    const u64 run = bitop3<0x20>(R, sum, O);    // R & ~sum & O
-    return and3(sum, R, P) ? run : 0ull;        // stop square is P
+// increasing bit order, the carry of X + mv, X = (O | ~R), starts at the move's
+// own bit (set in X: the move is not on its ray), ripples through the non-ray
+// bits up to R's first square, on through the opponent discs at the start of
+// the ray (and the non-ray bits between them), and stops on the first ray
+// square that is not an opponent disc, which it sets.  The opponent squares it
+// cleared are the run; they flip iff the stop square holds a P disc.  A run
+// that reaches the edge carries out of the ray: no stop square, no flips.
+// Round 5: the carry starts at mv, not at the ray's first square (six variable
+// 64-bit shifts fewer), and the diagonal rays are the shifted line patterns
+// unmasked, with O taken on the inner files only (Oi): an opponent disc on an
+// edge file can never be flanked along a diagonal, so the stop is at the
+// ray's edge square at the latest, before any square the pattern wraps to; a
+// move on the edge file, whose exact ray is empty, stops at once on a wrapped
+// square with an empty run.  That drops the two file masks and their
+// reversals (2 shifts, 2 adds, 4 v_bfrev, 8 v_bitop3).
+// The test is one 64-bit compare (v_cmp_ne_u64) and the select two
+// v_cndmask: hipcc ORs the two halves of the and3 and compares 32 bits.
+__device__ __forceinline__ u64 sel_nz(u64 t, u64 x) {  // t != 0 ? x : 0
+    u32 lo, hi;
+    u64 m;
+    asm("v_cmp_ne_u64_e64 %2, 0, %3\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %0, 0, %4, %2\n\t"
+        "v_cndmask_b32_e64 %1, 0, %5, %2"
+        : "=v"(lo), "=v"(hi), "=&s"(m)
+        : "v"(t), "v"((u32)x), "v"((u32)(x >> 32)));
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 ray_flips(u64 mv, u64 R, u64 P, u64 O) {
+    const u64 sum = add64(bfi(R, O, ~0ull), mv);  // (O | ~R) + mv
+    const u64 run = bitop3<0x20>(R, sum, O);      // R & ~sum & O
+    return sel_nz(and3(sum, R, P), run);          // stop square is P
 }
 
-// The six table rays of one square computed in registers (same rows as
-// ray_table_init): a shifted line pattern, masked to the files the ray can
-// reach.  Rows 3..5 are the decreasing rays in the bit-reversed layout, where
-// the square is 63 - sq and a file mask is the mirror (rev64) of its normal
-// counterpart.  ~20 VALU; the single-step kernel uses this instead of an LDS
-// table, whose per-block copy and barrier cost more than that
-// (tools/diag/launch_floor.py, step_ab.py), or a constant table in global
-// memory: six more vector loads per board cost the HBM-bound step 159 ->
-// 182 us per 16M boards (round 4, tools/diag/step_ab.py).
+// The six rays of one square in registers: rows 0..2 the increasing rays +8,
+// +9, +7, rows 3..5 the decreasing ones in the bit-reversed layout (square
+// 63 - sq).  The diagonals are the shifted line patterns, unmasked (see
+// ray_flips: their carries run over the inner-file opponent discs).  Six
+// v_lshlrev_b64; the single-step kernel uses this instead of an LDS table,
+// whose per-block copy and barrier cost more (tools/diag/launch_floor.py,
+// step_ab.py), or a constant table in global memory: six more vector loads
+// per board cost the HBM-bound step 159 -> 182 us per 16M boards (round 4).
 __device__ __forceinline__ void rays_of(u32 sq, u64 (&R)[kRayRows]) {
-    constexpr u64 ONES = 0x0101010101010101ull;
-    const u32 x = sq & 7u, rsq = sq ^ 63u;
-    const u64 le = (ONES << (x + 1)) - ONES;  // files <= x (x = 7: all)
-    const u64 lt = (ONES << x) - ONES;        // files < x
-    R[0] = 0x0101010101010100ull << sq;                            // +8
-    R[1] = andn(0x8040201008040200ull << sq, le);                  // +9: files > x
-    R[2] = and2(0x0002040810204080ull << sq, lt);                  // +7: files < x
-    R[3] = 0x0101010101010100ull << rsq;                           // -8
-    R[4] = and2(0x8040201008040200ull << rsq, rev64(lt));          // -9: normal files < x
-    R[5] = andn(0x0002040810204080ull << rsq, rev64(le));          // -7: normal files > x
+    const u32 rsq = sq ^ 63u;
+    R[0] = 0x0101010101010100ull << sq;   // +8
+    R[1] = 0x8040201008040200ull << sq;   // +9 (wraps past file h: see ray_flips)
+    R[2] = 0x0002040810204080ull << sq;   // +7 (wraps past file a)
+    R[3] = 0x0101010101010100ull << rsq;  // -8, reversed
+    R[4] = 0x8040201008040200ull << rsq;  // -9, reversed
+    R[5] = 0x0002040810204080ull << rsq;  // -7, reversed
 }
 
 // flips of the move on empty square sq (Board.put's count is their popcount,
-// board.py:161-174); 0 when nothing is flanked.  Horizontal runs by the carry
-// on the inner files (no ray mask needed), the six others by ray_flips; rays
-// leaving in decreasing bit order on the bit-reversed board.
+// board.py:161-174); 0 when nothing is flanked.  Exact for any disjoint own /
+// opponent pair (put_s_any's Empty side included).  Horizontal runs by the
+// carry on the inner files, the six others by ray_flips (the diagonals over
+// the inner files, the verticals over all); rays leaving in decreasing bit
+// order on the bit-reversed board.
 __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     u64 R[kRayRows];
     rays_of(sq, R);
@@ -396,12 +415,12 @@ __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
     const u64 rP = rev64(P), rO = rev64(O);
     const u64 Oi = and2(O, INNER_FILES), rOi = and2(rO, INNER_FILES);
     const u64 se = lshl1_add(mv, Oi), sw = lshl1_add(rmv, rOi);
-    u64 f = and2(se, P) ? andn(Oi, se) : 0ull;
-    u64 fr = and2(sw, rP) ? andn(rOi, sw) : 0ull;
-    f = or3(f, ray_flips(mv << 8, R[0], P, O), ray_flips(mv << 9, R[1], P, O));
-    f |= ray_flips(mv << 7, R[2], P, O);
-    fr = or3(fr, ray_flips(rmv << 8, R[3], rP, rO), ray_flips(rmv << 9, R[4], rP, rO));
-    fr |= ray_flips(rmv << 7, R[5], rP, rO);
+    u64 f = sel_nz(and2(se, P), andn(Oi, se));
+    u64 fr = sel_nz(and2(sw, rP), andn(rOi, sw));
+    f = or3(f, ray_flips(mv, R[0], P, O), ray_flips(mv, R[1], P, Oi));
+    f = or2(f, ray_flips(mv, R[2], P, Oi));
+    fr = or3(fr, ray_flips(rmv, R[3], rP, rO), ray_flips(rmv, R[4], rP, rOi));
+    fr = or2(fr, ray_flips(rmv, R[5], rP, rOi));
     return or2(f, rev64(fr));
 }
 

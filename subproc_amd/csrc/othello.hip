@@ -544,7 +544,32 @@ struct RolloutArgs {
     u32 n_rand_a, n_rand_b;
     int swap;
     uint8_t* a_black;
+    // OTH_HANDOFF builds (A/B): a fresh random batch hands its games over to the
+    // wave's LDS pool once no more than handoff_k lanes are still playing
+    u32 handoff_k;
 };
+
+// Batch-tail compaction (A/B builds only, OTH_HANDOFF=1; round 3's variant on
+// the round-4 kernel, the round-4 verdict's item 5).  When at most handoff_k
+// lanes of a fresh batch are still playing (a __ballot of the loop's live
+// lanes, __popcll), the wave parks those games -- the whole lane state, 32 B
+// -- in its LDS pool, compacted to the pool's top by mbcnt, and dequeues the
+// next batch; once 64 games are parked they are played out as a batch of their
+// own, and a wave that finds the queue empty plays out what it has parked.
+#ifndef OTH_HANDOFF
+#define OTH_HANDOFF 0
+#endif
+constexpr u32 kHandoffK = 16;                       // the default K (env OTH_HANDOFF_K)
+constexpr u32 kHandoffKMax = 16;                    // the pool's capacity allows K up to this
+constexpr int kPoolCap = 64 + (int)kHandoffKMax;    // < 64 parked + at most K more per batch
+struct Parked {
+    u64 P, O;        // the side to move's discs, the other side's
+    u32 state, inc;  // GameRng
+    u32 g;           // game index in the launch
+    u32 bits;        // b0 | passed << 1 | discs0 << 2 (7 bits) | npass << 9
+};
+static_assert(sizeof(Parked) == 32, "two 16-B LDS accesses per parked game");
+constexpr u64 kParkedGame = ~0ull;
 
 #ifdef OTH_DIAG
 __device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
@@ -586,6 +611,8 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     __shared__ u64 rays[kTabRows * 64];
     __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
+    constexpr bool kPool = OTH_HANDOFF && POLICY == OTH_POLICY_RANDOM && !RECORD && !RUNNER;
+    __shared__ Parked pool_s[kPool ? kBlock / 64 : 1][kPool ? kPoolCap : 1];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
     ray_table_init(rays);
@@ -603,18 +630,36 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
     uint8_t* const rec_wave = reinterpret_cast<uint8_t*>(rec_dyn) + (threadIdx.x >> 6) * kRecWaveBytes;
     uint8_t* const rec_row = rec_wave + lane * kRecStride;
 
+    Parked* const pool = pool_s[kPool ? threadIdx.x >> 6 : 0];
+    u32 parked = 0;          // wave-uniform: games in the wave's pool (kPool)
+    bool exhausted = false;  // wave-uniform: the wave has made its failing dequeue
+    (void)pool;
+    (void)exhausted;
     for (;;) {
-        // ---- dequeue a batch of 64 games (one per lane)
+        // ---- dequeue a batch of 64 games (one per lane), or (kPool) take the
+        // pool's parked games
+        bool from_pool = false;
         u64 base = 0;
-        if (lane == 0) {
-            base = atomicAdd(a.work, 64ull);
-            if (base == a.last_ticket) atomicExch(a.work, 0ull);  // every dequeue is done: reset
+        if (kPool && parked >= 64u) {
+            from_pool = true;
+        } else if (!kPool || !exhausted) {
+            if (lane == 0) {
+                base = atomicAdd(a.work, 64ull);
+                if (base == a.last_ticket) atomicExch(a.work, 0ull);  // every dequeue is done: reset
+            }
+            base = __shfl(base, 0);
+            if (base >= n) {  // wave-uniform
+                if (!kPool || parked == 0u) break;
+                exhausted = true;
+                from_pool = true;
+            }
+        } else {
+            if (parked == 0u) break;
+            from_pool = true;
         }
-        base = __shfl(base, 0);
-        if (base >= n) break;  // wave-uniform
 
-        const u64 g = base + lane;
-        bool active = g < n;
+        u64 g = base + lane;
+        bool active = !from_pool && g < n;
         u64 P = OPEN_BLACK, O = OPEN_WHITE;
         u32 side = OTH_BLACK, ply = 0;
         bool passed = false;
@@ -656,9 +701,30 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
             // swap.  Without a move record the ply counter is not kept either:
             // every placement adds one disc, so plies = discs placed + passes
             // handed over (a pass just before the terminal is not an env-step).
-            const bool b0 = side == OTH_BLACK;
-            const u32 discs0 = RECORD ? 0u : (u32)__popcll(P | O);
+            bool b0 = side == OTH_BLACK;
+            u32 discs0 = RECORD ? 0u : (u32)__popcll(P | O);
             u32 npass = 0;  // passes (RECORD: every ply)
+            if (kPool && from_pool) {  // the top (up to) 64 parked games
+                const u32 take = min(parked, 64u);
+                active = (u32)lane < take;
+                if (active) {
+                    const Parked e = pool[parked - take + lane];
+                    P = e.P;
+                    O = e.O;
+                    rng.state = e.state;
+                    rng.inc = e.inc;
+                    g = e.g;
+                    b0 = e.bits & 1u;
+                    passed = (e.bits >> 1) & 1u;
+                    discs0 = (e.bits >> 2) & 0x7fu;
+                    npass = e.bits >> 9;
+                }
+                parked -= take;
+            }
+            const u32 hand_k = __builtin_amdgcn_readfirstlane(kPool && !from_pool ? a.handoff_k : 0u);
+            const u32 parked0 = __builtin_amdgcn_readfirstlane(parked);
+            (void)hand_k;
+            (void)parked0;
             // one ply of mover X against Y; true at the terminal.  The
             // terminal's bookkeeping (final board, diff, plies, histogram) is
             // done once per lane after the loop, where P is still side0's
@@ -704,7 +770,25 @@ __global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  //
                 for (;;) {
                     if (ply_of(P, O)) break;
                     if (ply_of(O, P)) break;
+                    if (kPool) {  // the batch's tail: park the lanes still playing
+                        const u64 live = __ballot(1);
+                        if ((u32)__popcll(live) <= hand_k) {
+                            const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(live >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((u32)live, 0u));
+                            pool[parked0 + rank] = Parked{P, O, rng.state, rng.inc, (u32)g,
+                                                          (u32)b0 | (u32)passed << 1 | discs0 << 2 | npass << 9};
+                            g = kParkedGame;
+                            break;
+                        }
+                    }
                 }
+            }
+            if (kPool) {
+                const u64 pm = __ballot(active && g == kParkedGame);
+                parked = parked0 + (u32)__popcll(pm);
+                if (g == kParkedGame) active = false;
+            }
+            if (active) {
                 const u32 ply = RECORD ? npass : (u32)__popcll(P | O) - discs0 + npass;
                 if (RECORD) rec_put(ply, 0xFF);
                 const u64 bl = b0 ? P : O, wh = b0 ? O : P;
@@ -2108,6 +2192,10 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     // (lane_choose), so the per-lane path runs from ordinary positions
     a.coop_cap = env_int("OTH_COOP_CAP", 1) == 0 ? 0u : 1u;
     a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
+    // (OTH_HANDOFF builds: game indices are parked as 32 bits)
+    a.handoff_k = OTH_HANDOFF && n <= 0xFFFFFFFFll
+                      ? (u32)std::min(std::max(env_int("OTH_HANDOFF_K", (int)kHandoffK), 0), (int)kHandoffKMax)
+                      : 0u;
     hipStream_t st = (hipStream_t)stream;
     if (run) {
         if (policy == OTH_POLICY_EVAL) {

@@ -58,6 +58,483 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
     values[i] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
 }
 
+// ---------------------------------------------------------------------------
+// The grouping sort (oth_td_sort_packed / oth_td_sort_unpack): a stable LSD
+// radix sort of 64-bit words by their low `bits` bits, written for gfx950 in
+// the onesweep form -- one read and one write of the words per digit:
+//   * sort_hist_kernel: one read of the input, the histograms of every
+//     digit position at once (LDS counters per block, then global atomics);
+//   * sort_pass_kernel, once per digit: a block takes the next tile of
+//     kSortTile words (an atomic ticket, so tiles start in order), ranks
+//     them stably in LDS, publishes its per-digit counts and looks back over
+//     the tiles before it for their running totals (decoupled look-back, one
+//     flag word per tile polled 64 tiles at a time; below),
+//     then writes the tile out digit by digit through an LDS stage, so
+//     consecutive lanes store consecutive words of one digit's run.
+//     (n < 2^32: the counts are 32-bit.)
+// Ranking: a wave ranks its 64 words of a round by ballots over the digit's
+// bits (the lanes with the same digit: `peers`), the lane's place among them
+// by mbcnt, and the wave's running count of the digit in LDS, read by every
+// lane and bumped by the lowest lane of each peer group (one wave's LDS
+// instructions execute in order, so each round sees the last one's counts).
+// Words keep their order: within a wave by round then lane, across the
+// block's waves by the waves' prefix counts, across tiles by the look-back.
+// The last pass can write the unpacked (key, value) pairs straight away
+// (oth_td_sort_unpack: oth_td_unpack fused in).
+#ifndef OTH_SORT_ROCPRIM  // 1: rocPRIM's onesweep (the shipped build while the own sort trails it)
+#define OTH_SORT_ROCPRIM 1
+#endif
+#ifndef OTH_SORT_DIGIT
+#define OTH_SORT_DIGIT 9
+#endif
+#ifndef OTH_SORT_WAVES
+#define OTH_SORT_WAVES 4
+#endif
+#ifndef OTH_SORT_ROUNDS
+#define OTH_SORT_ROUNDS 16
+#endif
+#ifndef OTH_SORT_DIGIT_WALK
+#define OTH_SORT_DIGIT_WALK 0
+#endif
+#ifndef OTH_SORT_NEAR
+#define OTH_SORT_NEAR 4
+#endif
+#ifndef OTH_SORT_WAITFAR
+#define OTH_SORT_WAITFAR 32
+#endif
+constexpr int kSortNear = OTH_SORT_NEAR, kSortWaitFar = OTH_SORT_WAITFAR;
+// diagnostic builds only (wrong output, for timing the parts): no look-back;
+// the tile written back in place, unscattered
+#ifndef OTH_SORT_DIAG_NOLOOK
+#define OTH_SORT_DIAG_NOLOOK 0
+#endif
+#ifndef OTH_SORT_DIAG_LINEAR
+#define OTH_SORT_DIAG_LINEAR 0
+#endif  // look-back window (tiles per digit in flight)
+constexpr int kSortDigitBits = OTH_SORT_DIGIT;
+constexpr int kSortDigits = 1 << kSortDigitBits;
+constexpr int kSortWaves = OTH_SORT_WAVES;
+constexpr int kSortRounds = OTH_SORT_ROUNDS;
+constexpr int kSortThreads = 64 * kSortWaves;
+constexpr int kSortTile = kSortThreads * kSortRounds;
+constexpr int kSortMaxPasses = (64 + kSortDigitBits - 1) / kSortDigitBits;
+constexpr int kSortHistBlock = 256;
+static_assert(kSortDigits % kSortThreads == 0, "digits per thread");
+constexpr int kSortDigitsPerThread = kSortDigits / kSortThreads;
+
+// the digit of pass q: bits [q * D, min((q + 1) * D, bits)) -- the last
+// pass's digit is narrower when D does not divide `bits` (the bits above are
+// the packed word's payload, which must not order anything)
+__device__ __forceinline__ uint32_t sort_digit(uint64_t w, int shift, uint32_t mask) {
+    return (uint32_t)(w >> shift) & mask;
+}
+__host__ __device__ __forceinline__ uint32_t sort_mask(int bits, int q) {
+    const int w = bits - q * kSortDigitBits;
+    return w >= kSortDigitBits ? (uint32_t)(kSortDigits - 1) : (1u << w) - 1u;
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// inclusive scan of x over the wave's 64 lanes (DPP row shifts and row broadcasts)
+__device__ __forceinline__ uint32_t sort_wave_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// the histograms of every digit position: hist[p * kSortDigits + d] (zeroed
+// by the launcher)
+// (kSortHistCopies copies of the counters, lanes spread over them: a wave's
+// lanes with the same digit -- the disc field of the opening plies, say --
+// serialise on one LDS address otherwise; dynamic LDS, copies x passes x
+// digits words).  Each thread reads two words per 16-byte load, four loads in
+// flight.
+#ifndef OTH_SORT_HIST_COPIES
+#define OTH_SORT_HIST_COPIES 4
+#endif
+constexpr int kSortHistCopies = OTH_SORT_HIST_COPIES;
+__global__ __launch_bounds__(kSortHistBlock) void sort_hist_kernel(const uint64_t* __restrict__ in, int64_t n,
+                                                                   int passes, int bits,
+                                                                   unsigned long long* __restrict__ hist) {
+    extern __shared__ uint32_t hdyn[];
+    const int per = passes * kSortDigits;
+    for (int e = threadIdx.x; e < kSortHistCopies * per; e += kSortHistBlock) hdyn[e] = 0;
+    __syncthreads();
+    uint32_t* hc = hdyn + (threadIdx.x & (kSortHistCopies - 1)) * per;
+    auto count = [&](uint64_t w) {
+        for (int p = 0; p < passes; p++)
+            atomicAdd(&hc[p * kSortDigits + sort_digit(w, p * kSortDigitBits, sort_mask(bits, p))], 1u);
+    };
+    // a word before the first 16-byte boundary (a caller's offset pointer)
+    // alone, then pairs, then a last odd word
+    const int lead = (reinterpret_cast<uintptr_t>(in) & 15) ? 1 : 0;
+    if (lead && n > 0 && blockIdx.x == 0 && threadIdx.x == 0) count(in[0]);
+    const int64_t n2 = (n - lead) >> 1;  // word pairs
+    const ulonglong2* in2 = reinterpret_cast<const ulonglong2*>(in + lead);
+    const int64_t stride = (int64_t)gridDim.x * kSortHistBlock;
+    int64_t i = (int64_t)blockIdx.x * kSortHistBlock + threadIdx.x;
+    for (; i + 3 * stride < n2; i += 4 * stride) {
+        ulonglong2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = in2[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            count(v[u].x);
+            count(v[u].y);
+        }
+    }
+    for (; i < n2; i += stride) {
+        const ulonglong2 v = in2[i];
+        count(v.x);
+        count(v.y);
+    }
+    if (((n - lead) & 1) && blockIdx.x == 0 && threadIdx.x == 0) count(in[n - 1]);
+    __syncthreads();
+    for (int e = threadIdx.x; e < per; e += kSortHistBlock) {
+        uint32_t c = 0;
+        for (int k = 0; k < kSortHistCopies; k++) c += hdyn[k * per + e];
+        if (c) atomicAdd(&hist[e], (unsigned long long)c);
+    }
+}
+
+// One digit pass (see above).  UNPACK: write keys_out / vals_out (the word's
+// low OTH_TD_KEY_BITS, and value_side * lam_pow[turn_left]) instead of out.
+template <bool UNPACK>
+__global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
+    const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int64_t n, int shift, uint32_t dmask, uint32_t tag,
+    const unsigned long long* __restrict__ hist, unsigned* __restrict__ status, size_t vec_off,
+    unsigned* __restrict__ ticket, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
+    double* __restrict__ vals_out) {
+    __shared__ uint64_t stage[kSortTile];
+    __shared__ uint32_t wcnt[kSortWaves][kSortDigits];  // a wave's running counts, then its prefix over waves
+    __shared__ uint32_t blk_off[kSortDigits];           // the tile's digits: exclusive prefix of their counts
+    __shared__ long long gbase[kSortDigits];            // output index of the tile's slot 0, per digit
+    __shared__ uint32_t wsum[kSortWaves];
+    __shared__ unsigned long long hsum[kSortWaves];
+    __shared__ uint32_t tile_s, look_k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid == 0) tile_s = atomicAdd(ticket, 1u);
+    for (int e = tid; e < kSortWaves * kSortDigits; e += kSortThreads) (&wcnt[0][0])[e] = 0;
+    __syncthreads();
+    const int64_t tile = tile_s;
+    const int64_t t0 = tile * kSortTile, wbase = t0 + (int64_t)wave * (kSortRounds * 64);
+    // the wave's words, every round's load in flight before the first is ranked
+    uint64_t v[kSortRounds];
+#pragma unroll
+    for (int k = 0; k < kSortRounds; k++) {
+        const int64_t i = wbase + k * 64 + lane;
+        v[k] = i < n ? in[i] : 0ull;
+    }
+    volatile uint32_t* wc = wcnt[wave];
+    uint32_t rank[kSortRounds];
+#pragma unroll
+    for (int k = 0; k < kSortRounds; k++) {
+        const bool valid = wbase + k * 64 + lane < n;
+        const uint32_t d = sort_digit(v[k], shift, dmask);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kSortDigitBits; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t below = lanes_below(peers);
+        const uint32_t old = valid ? wc[d] : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (valid && below == 0) wc[d] = old + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        rank[k] = old + below;
+    }
+    __syncthreads();
+    // per digit: the waves' exclusive prefix (in place) and the tile's count;
+    // the global offset of the digit (exclusive scan of this pass's histogram)
+    uint32_t tot[kSortDigitsPerThread];
+    unsigned long long hcnt[kSortDigitsPerThread];
+    uint32_t tsum = 0;
+    unsigned long long hs = 0;
+#pragma unroll
+    for (int j = 0; j < kSortDigitsPerThread; j++) {
+        const int d = tid * kSortDigitsPerThread + j;
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < kSortWaves; w++) {
+            const uint32_t c = wcnt[w][d];
+            wcnt[w][d] = s;
+            s += c;
+        }
+        tot[j] = s;
+        tsum += s;
+        hcnt[j] = hist[d];
+        hs += hcnt[j];
+    }
+    // exclusive scans over the digits (thread-major: thread t owns digits
+    // t*DPT .. t*DPT+DPT-1): the tile's counts and the pass histogram
+    const uint32_t ti = sort_wave_scan(tsum);
+    unsigned long long hi = hs;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(hi, o);
+        if (lane >= o) hi += y;
+    }
+    if (lane == 63) {
+        wsum[wave] = ti;
+        hsum[wave] = hi;
+    }
+    __syncthreads();
+    uint32_t tpre = ti - tsum;
+    unsigned long long hpre = hi - hs;
+    for (int w = 0; w < wave; w++) {
+        tpre += wsum[w];
+        hpre += hsum[w];
+    }
+#if OTH_SORT_DIGIT_WALK
+    // (A/B) each digit's chain walked by its own thread, the status words laid
+    // out [digit][tile] so that a walk reads consecutive words
+    unsigned long long acc[kSortDigitsPerThread];
+    {
+        uint64_t* dw = reinterpret_cast<uint64_t*>(status + vec_off);
+        const int64_t nt = gridDim.x;
+        const uint64_t tagw = (uint64_t)tag << 56;
+        bool open[kSortDigitsPerThread];
+        int64_t tl[kSortDigitsPerThread];
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++) {
+            const int d = tid * kSortDigitsPerThread + j;
+            __hip_atomic_store(dw + d * nt + tile, ((tile ? 1ull : 2ull) << 62) | tagw | tot[j], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            acc[j] = 0;
+            open[j] = tile > 0;
+            tl[j] = tile - 1;
+        }
+        for (;;) {
+            bool any = false;
+            uint64_t x[kSortDigitsPerThread];
+#pragma unroll
+            for (int j = 0; j < kSortDigitsPerThread; j++) {
+                const int d = tid * kSortDigitsPerThread + j;
+                x[j] = open[j] ? __hip_atomic_load(dw + d * nt + tl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < kSortDigitsPerThread; j++) {
+                if (!open[j]) continue;
+                if (((x[j] >> 56) & 63u) == tag && (x[j] >> 62) != 0) {
+                    acc[j] += x[j] & ((1ull << 56) - 1);
+                    if ((x[j] >> 62) == 2) open[j] = false;
+                    else tl[j]--;
+                }
+                any |= open[j];
+            }
+            if (!any) break;
+        }
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++) {
+            const int d = tid * kSortDigitsPerThread + j;
+            if (tile)
+                __hip_atomic_store(dw + d * nt + tile, (2ull << 62) | tagw | (acc[j] + tot[j]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#else
+    // publish the tile's counts, look back over the tiles before it, publish
+    // the inclusive counts.  Status: one 64-bit word per (tile, digit),
+    //   flag (1 = the tile's own count, 2 = inclusive of every tile before it)
+    //   << 62 | pass tag << 56 | count,
+    // self-validating, so no fence orders anything: a reader takes a word only
+    // once its tag is this pass's and its flag is set.  And one hint word per
+    // tile (tag << 2 | the same flag), stored after the tile's words, which
+    // wave 0 polls for the 64 tiles before it at once to find how far back the
+    // nearest inclusive tile lies; every thread then loads its digits' words of
+    // those tiles together, re-polling a word not yet visible, and stops at its
+    // first inclusive one.  (Round 5's first version walked each digit's chain
+    // on its own thread, tile by tile: 1.4 ms of a 2.3 ms sort.  A flag per
+    // tile over plain count vectors needs a release fence per tile, which on
+    // gfx950 writes back the XCD's whole L2, the sort's scattered output
+    // included: 3-5 ms.)
+    uint32_t* hint = status;
+    uint64_t* word = reinterpret_cast<uint64_t*>(status + vec_off);
+    uint64_t* mine = word + (size_t)tile * kSortDigits;
+    const uint64_t tagw = (uint64_t)tag << 56;
+#pragma unroll
+    for (int j = 0; j < kSortDigitsPerThread; j++)
+        __hip_atomic_store(mine + tid * kSortDigitsPerThread + j, ((tile ? 1ull : 2ull) << 62) | tagw | tot[j],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (tid == 0)
+        __hip_atomic_store(hint + tile, (tag << 2) | (tile ? 1u : 2u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long acc[kSortDigitsPerThread];
+    bool open[kSortDigitsPerThread];
+#pragma unroll
+    for (int j = 0; j < kSortDigitsPerThread; j++) {
+        acc[j] = 0;
+        open[j] = tile > 0 && !OTH_SORT_DIAG_NOLOOK;
+    }
+    int64_t hi_t = tile - 1;  // the nearest predecessor not yet summed
+    while (hi_t >= 0 && !OTH_SORT_DIAG_NOLOOK) {
+        if (wave == 0) {
+            uint32_t k = 0, polls = 0;
+            for (;; polls++) {
+                const int64_t t = hi_t - lane;
+                const uint32_t f =
+                    t >= 0 ? __hip_atomic_load(hint + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                const bool ready = (f >> 2) == tag && (f & 3u) != 0;
+                const uint64_t mr = __ballot(ready), mi = __ballot(ready && (f & 3u) == 2u);
+                const uint32_t first_gap = mr == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mr);
+                const uint32_t near_inc = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
+                // an inclusive tile within kSortNear: its own counts and the
+                // tiles' between; farther back, wait up to kSortWaitFar polls
+                // for the inclusive front to come closer (the first wave of
+                // blocks would each read hundreds of tiles' counts), then sum
+                // what is published
+                const bool patient = polls < (uint32_t)kSortWaitFar;
+                if (near_inc < first_gap && (near_inc < (uint32_t)kSortNear || !patient)) {
+                    k = near_inc + 1;
+                    break;
+                }
+                if (first_gap > 0 && !patient) {  // own counts only: sum them, look further back
+                    k = first_gap;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) look_k = k;
+        }
+        __syncthreads();
+        const int64_t k = look_k;
+        for (int64_t i = 0; i < k; i++) {
+            const uint64_t* tw = word + (size_t)(hi_t - i) * kSortDigits + tid * kSortDigitsPerThread;
+            uint64_t x[kSortDigitsPerThread];
+#pragma unroll
+            for (int j = 0; j < kSortDigitsPerThread; j++)
+                x[j] = open[j] ? __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+            for (int j = 0; j < kSortDigitsPerThread; j++) {
+                if (!open[j]) continue;
+                // (the hint may be visible before the word: poll it.  A word
+                // still holding the tile's own count where the hint said
+                // inclusive is summed as such, and the walk goes on.)
+                while (((x[j] >> 56) & 63u) != tag || (x[j] >> 62) == 0)
+                    x[j] = __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                acc[j] += x[j] & ((1ull << 56) - 1);
+                if ((x[j] >> 62) == 2) open[j] = false;
+            }
+        }
+        hi_t -= k;
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++) any |= open[j];
+        if (!__syncthreads_or(any)) break;  // every digit reached an inclusive count
+    }
+    if (tile) {
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++)
+            __hip_atomic_store(mine + tid * kSortDigitsPerThread + j, (2ull << 62) | tagw | (acc[j] + tot[j]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(hint + tile, (tag << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+#pragma unroll
+    for (int j = 0; j < kSortDigitsPerThread; j++) {
+        const int d = tid * kSortDigitsPerThread + j;
+        blk_off[d] = tpre;
+        gbase[d] = (long long)(hpre + acc[j]) - (long long)tpre;
+        tpre += tot[j];
+        hpre += hcnt[j];
+    }
+    __syncthreads();
+    // the tile in digit order in LDS
+#pragma unroll
+    for (int k = 0; k < kSortRounds; k++) {
+        if (wbase + k * 64 + lane < n) {
+            const uint32_t d = sort_digit(v[k], shift, dmask);
+            stage[blk_off[d] + wcnt[wave][d] + rank[k]] = v[k];
+        }
+    }
+    __syncthreads();
+    const int nv = (int)min<int64_t>(kSortTile, n - t0);
+#pragma unroll 4
+    for (int s = tid; s < nv; s += kSortThreads) {
+        const uint64_t w = stage[s];
+        const int64_t pos = OTH_SORT_DIAG_LINEAR ? t0 + s : gbase[sort_digit(w, shift, dmask)] + s;
+        if (UNPACK) {
+            const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
+            keys_out[pos] = (int64_t)(w & ((1ull << OTH_TD_KEY_BITS) - 1));
+            vals_out[pos] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
+        } else {
+            out[pos] = w;
+        }
+    }
+}
+
+// scratch: [ping-pong words (n) | histograms | tickets | status (tiles x digits)]
+struct SortPlan {
+    int passes;
+    int64_t tiles;
+    size_t words_off, hist_off, ticket_off, status_off, vec_off, bytes;
+};
+inline SortPlan sort_plan(int64_t n, int bits) {
+    SortPlan p;
+    p.passes = (bits + kSortDigitBits - 1) / kSortDigitBits;
+    p.tiles = (n + kSortTile - 1) / kSortTile;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    p.words_off = 0;
+    p.hist_off = al((size_t)n * sizeof(uint64_t));
+    p.ticket_off = al(p.hist_off + (size_t)p.passes * kSortDigits * sizeof(unsigned long long));
+    p.status_off = al(p.ticket_off + (size_t)p.passes * sizeof(unsigned));
+    // status: the tiles' hint words, then their (tile, digit) words (vec_off:
+    // in 32-bit units, even)
+    const size_t tiles = (size_t)std::max<int64_t>(p.tiles, 1);
+    p.vec_off = (tiles + 63) / 64 * 64;
+    p.bytes = al(p.status_off + (p.vec_off + tiles * 2 * kSortDigits) * sizeof(uint32_t));
+    return p;
+}
+// the sort of n words by bits [0, bits): into out (keys NULL) or unpacked into
+// keys / vals; temp of sort_plan(n, bits).bytes
+hipError_t sort_words(const uint64_t* in, uint64_t* out, int64_t n, int bits, const double* lam_pow, int64_t* keys,
+                      double* vals, void* temp, hipStream_t st) {
+    const SortPlan p = sort_plan(n, bits);
+    char* t = static_cast<char*>(temp);
+    uint64_t* tmp = reinterpret_cast<uint64_t*>(t + p.words_off);
+    unsigned long long* hist = reinterpret_cast<unsigned long long*>(t + p.hist_off);
+    unsigned* ticket = reinterpret_cast<unsigned*>(t + p.ticket_off);
+    unsigned* status = reinterpret_cast<unsigned*>(t + p.status_off);
+    // histograms, tickets and every status word start at 0 (one fill per
+    // sort: the pass tags tell this sort's passes apart, the fill any earlier
+    // use of the scratch)
+    hipError_t e = hipMemsetAsync(t + p.hist_off, 0, p.bytes - p.hist_off, st);
+    if (e != hipSuccess) return e;
+    sort_hist_kernel<<<512, kSortHistBlock, kSortHistCopies * p.passes * kSortDigits * sizeof(uint32_t), st>>>(
+        in, n, p.passes, bits, hist);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the passes ping-pong so that the last one writes the output: words into
+    // `out` and tmp; unpacked, the words through tmp and the keys array
+    uint64_t* bufA = keys ? reinterpret_cast<uint64_t*>(keys) : out;
+    uint64_t* bufB = tmp;
+    const uint64_t* src = in;
+    for (int q = 0; q < p.passes; q++) {
+        const bool last = q == p.passes - 1;
+        // the destination of pass q: the buffers alternate so that the last
+        // pass lands in `out` (or the unpacked arrays)
+        uint64_t* dst = ((p.passes - 1 - q) & 1) ? bufB : bufA;
+        if (keys && last) dst = nullptr;
+        if (keys && last)
+            sort_pass_kernel<true><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
+                src, nullptr, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
+                p.vec_off, ticket + q, lam_pow, keys, vals);
+        else
+            sort_pass_kernel<false><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
+                src, dst, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
+                p.vec_off, ticket + q, nullptr, nullptr, nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        src = dst;
+    }
+    return hipSuccess;
+}
+
 constexpr int kMergeBlock = 256;
 #ifndef OTH_MERGE_K  // A/B builds only
 #define OTH_MERGE_K 8
@@ -591,6 +1068,7 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream) {
     if (n < 0 || !temp_bytes) return OTH_EINVAL;
+#if OTH_SORT_ROCPRIM
     if (!temp) {  // size query: no work, no launch
         size_t bytes = 0;
         const hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, bytes, words_in, words_out, (size_t)n,
@@ -603,6 +1081,58 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     size_t bytes = *temp_bytes;
     const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
                                                               0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+#else
+    const size_t need = sort_plan(n, OTH_TD_KEY_BITS).bytes;
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (n > 0 && (!words_in || !words_out || words_in == words_out)) return OTH_EINVAL;
+    if (n >= (1ll << 32)) return OTH_EINVAL;  // 32-bit counts
+    if (*temp_bytes < need) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+    const hipError_t e = sort_words(words_in, words_out, n, OTH_TD_KEY_BITS, nullptr, nullptr, nullptr, temp,
+                                    (hipStream_t)stream);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+#endif
+}
+
+int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t* keys, double* values, int64_t n,
+                       void* temp, size_t* temp_bytes, void* stream) {
+    if (n < 0 || !temp_bytes) return OTH_EINVAL;
+#if OTH_SORT_ROCPRIM
+    // rocPRIM's sort of the words into the scratch, then the unpack kernel
+    size_t sort_bytes = 0;
+    hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, sort_bytes, words_in, (uint64_t*)nullptr, (size_t)n,
+                                                        0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+    if (e != hipSuccess) return -(int)e;
+    sort_bytes = (sort_bytes + 255) / 256 * 256;
+    const size_t need = sort_bytes + (size_t)std::max<int64_t>(n, 1) * sizeof(uint64_t);
+#else
+    const size_t need = sort_plan(n, OTH_TD_KEY_BITS).bytes;
+#endif
+    if (!temp) {  // size query: no work, no launch
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (n > 0 && (!words_in || !lam_pow || !keys || !values ||
+                  reinterpret_cast<const void*>(words_in) == reinterpret_cast<const void*>(keys)))
+        return OTH_EINVAL;
+    if (n >= (1ll << 32)) return OTH_EINVAL;  // 32-bit counts
+    if (*temp_bytes < need) return OTH_EINVAL;
+    if (n == 0) return OTH_OK;
+#if OTH_SORT_ROCPRIM
+    uint64_t* sorted = reinterpret_cast<uint64_t*>(static_cast<char*>(temp) + sort_bytes);
+    e = rocprim::radix_sort_keys<SortConfig>(temp, sort_bytes, words_in, sorted, (size_t)n, 0, OTH_TD_KEY_BITS,
+                                             (hipStream_t)stream);
+    if (e != hipSuccess) return -(int)e;
+    td_unpack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(sorted, lam_pow, keys, values, n);
+    e = hipGetLastError();
+#else
+    const hipError_t e = sort_words(words_in, nullptr, n, OTH_TD_KEY_BITS, lam_pow, keys, values, temp,
+                                    (hipStream_t)stream);
+#endif
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 

@@ -163,15 +163,13 @@ class StateMap:
                                             None if row_off is None else row_off.contiguous().data_ptr(),
                                             plies.contiguous().data_ptr(), base.data_ptr(), words.data_ptr(), n,
                                             stream), "oth_td_updates_packed")
-            sorted_words = torch.empty_like(words)
-            _with_scratch(lib.oth_td_sort_packed, (words.data_ptr(), sorted_words.data_ptr(), total), stream,
-                          self.device, "oth_td_sort_packed")
-            del words
+            # the build's radix sort by key bits, its last pass writing the keys
+            # and values (oth_td_sort_unpack: the sort and the unpack in one)
             sk = torch.empty(total, dtype=torch.int64, device=self.device)
             sv = torch.empty(total, dtype=torch.float64, device=self.device)
-            check(lib.oth_td_unpack(sorted_words.data_ptr(), self._lam_pow.data_ptr(), sk.data_ptr(), sv.data_ptr(),
-                                    total, stream), "oth_td_unpack")
-            del sorted_words
+            _with_scratch(lib.oth_td_sort_unpack, (words.data_ptr(), self._lam_pow.data_ptr(), sk.data_ptr(),
+                                                   sv.data_ptr(), total), stream, self.device, "oth_td_sort_unpack")
+            del words
         self._apply_sorted(sk, sv)
         return total
 

@@ -6,11 +6,12 @@ Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
   * on gfx950 FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced
     streaming read: fetch_bytes_corrected = 2 * FETCH_SIZE * 1024 (an upper
     estimate for narrower accesses, which the guide leaves uncalibrated);
-  * SQ_ACTIVE_INST_VALU counts quad-cycles; SQ_BUSY_CYCLES is summed over the
-    32 shader engines: valu_busy = 4 * ACTIVE_INST_VALU / (1024 SIMDs * BUSY/32)
-    prices every VALU instruction at 4 cycles, so it can pass 1 when part of the
-    mix is plain VOP2 logic (~2.2 cycles); the mix-weighted ceiling is in
-    profiles/valu_mix.json (tools/valu_mix.py).
+  * valu_issue_frac = 2 * SQ_INSTS_VALU / (1024 SIMDs * gpu_cycles_pmc): the
+    fraction of the hardware's issue peak (one wave64 VALU instruction per SIMD
+    every 2 cycles, MI355X_MICROARCH.md) the dispatch used, which cannot pass
+    1.  (Rounds 1-4 published valu_busy = 4 * SQ_ACTIVE_INST_VALU / SIMD
+    cycles, which priced every instruction at 4 cycles and passed 1 for mixes
+    with fast logic; it is no longer reported.)
 """
 import collections
 import csv
@@ -96,12 +97,12 @@ def main(d):
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE"):
             if c in cs:
                 e[c] = cs[c]
-        if "SQ_ACTIVE_INST_VALU" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"] > 0:
-            e["valu_busy"] = 4 * cs["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cs["SQ_BUSY_CYCLES"] / N_SE)
         if "GRBM_GUI_ACTIVE" in cs:
             # GPU cycles of the (serialized) PMC dispatch; not divided by the kernel-trace
             # duration, which overlaps a neighbouring launch in the two-stream bench
             e["gpu_cycles_pmc"] = cs["GRBM_GUI_ACTIVE"] / 8
+            if "SQ_INSTS_VALU" in cs and e["gpu_cycles_pmc"] > 0:
+                e["valu_issue_frac"] = 2 * cs["SQ_INSTS_VALU"] / (N_SIMD * e["gpu_cycles_pmc"])
         out["kernels"][f"{k}@{grid}"] = e
     out["kernel_stats"] = stats
     json.dump(out, sys.stdout, indent=1)

@@ -666,30 +666,41 @@ def _bench_books(ops, torch, dev, args, games=1 << 18, reps=10):
     return out
 
 
-def _bench_td(ops, torch, dev, args, games=1 << 18):
+def _bench_td(ops, torch, dev, args, games=1 << 18, reps=7):
     """§8f row 2: the learner's TD state-map update for a batch of GPU self-play
     books (packed replay + ordered update stream + stable sort + per-key EMA +
-    merge into a table that already holds two batches)."""
+    merge into a table that already holds two batches).  The third batch is
+    applied `reps` times, each time to a fresh copy of the two-batch table (the
+    copy outside the timed region), and the median is reported (round 5: the
+    round-4 line timed one application once)."""
+    import statistics
+
     from subproc_amd.td import StateMap
 
     rs = [ops.rollout(games, args.seed, (1 << 41) + k * games, "random", record_moves=True, device=dev)
           for k in range(3)]
     sm = StateMap(dev)
-    for r in rs[:2]:  # warm-up: the empty-table path, then the merge path (first-use kernel loading)
+    for r in rs[:2]:  # the empty-table path, then the merge path (first-use kernel loading)
         pk = ops.replay_rows(r.moves, r.plies)
         sm.update(pk.boards, r.plies, pk.row_off)
-    torch.cuda.synchronize()
+    base_k, base_v = sm.keys.clone(), sm.values.clone()
     r2 = rs[2]
-    t0 = time.perf_counter()
-    # the books as GameBooks holds them: the packed replay (each game's recorded
-    # rows only), then the update over those rows (round 3 timed the strided
-    # replay, all 129 rows per game)
-    pk = ops.replay_rows(r2.moves, r2.plies)
-    n_upd = sm.update(pk.boards, r2.plies, pk.row_off)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    times, n_upd = [], 0
+    for _ in range(reps + 1):  # the first application warms the merge path at this size
+        sm.keys, sm.values = base_k.clone(), base_v.clone()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        # the books as GameBooks holds them: the packed replay (each game's
+        # recorded rows only), then the update over those rows
+        pk = ops.replay_rows(r2.moves, r2.plies)
+        n_upd = sm.update(pk.boards, r2.plies, pk.row_off)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    times = times[1:]
+    dt = statistics.median(times)
     return {"metric": "TD state-map updates/sec (position x side, learner order)", "value": n_upd / dt,
-            "unit": "updates/s", "games": games, "updates": n_upd, "keys": len(sm), "ms": dt * 1e3}
+            "unit": "updates/s", "games": games, "updates": n_upd, "keys": len(sm), "ms": dt * 1e3,
+            "ms_min": min(times) * 1e3, "ms_max": max(times) * 1e3, "reps": reps, "stat": "median"}
 
 
 def _cpu_baseline(args, workload):

@@ -358,6 +358,14 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
  * nonzero (and their two host syncs). */
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
                     int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream);
+/* oth_td_segments over the key-sorted packed words themselves (each read as
+ * its low OTH_TD_KEY_BITS), also writing values[i] = value_side *
+ * lam_pow[turn_left] of word i (oth_td_unpack's rule), so a sorted word
+ * stream needs no unpack pass: the keys array oth_td_segments reads is never
+ * formed (round 5).  values: n doubles (device); the rest as oth_td_segments. */
+int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t n, int64_t long_min, int64_t* seg_off,
+                          int64_t* ukeys, int64_t* long_idx, int64_t* counts, double* values, void* temp,
+                          size_t* temp_bytes, void* stream);
 
 /* new_before[j] = the number of nonzero is_new[0..j) for j = 0..n (n + 1
  * entries, device): oth_td_merge's new_before from oth_td_lookup's is_new.

@@ -392,6 +392,26 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
     return OTH_OK;
 }
 
+/* the segments of the sorted words' keys (temp: the keys, n int64), and the
+ * words' values by oth_td_unpack */
+int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t n, int64_t long_min, int64_t* seg_off,
+                          int64_t* ukeys, int64_t* long_idx, int64_t* counts, double* values, void* temp,
+                          size_t* temp_bytes, void* stream) {
+    if (n < 0 || long_min < 1 || !temp_bytes) return OTH_EINVAL;
+    const size_t need = (size_t)(n > 0 ? n : 1) * sizeof(int64_t);
+    if (!temp) {
+        *temp_bytes = need;
+        return OTH_OK;
+    }
+    if (*temp_bytes < need || !seg_off || !counts || (n > 0 && (!words || !lam_pow || !ukeys || !long_idx || !values)))
+        return OTH_EINVAL;
+    int64_t* keys = (int64_t*)temp;
+    size_t none = 0;
+    int rc = oth_td_unpack(words, lam_pow, keys, values, n, stream);
+    if (rc == OTH_OK) rc = oth_td_segments(keys, n, long_min, seg_off, ukeys, long_idx, counts, keys, &none, stream);
+    return rc;
+}
+
 /* stable sort of (key, value) pairs by key: bottom-up merge sort of the pair
  * indices (temp holds 2 * n int64 indices), then a gather */
 int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* keys_out, double* vals_out, int64_t n,

@@ -51,6 +51,7 @@ SIGNATURES = {
     "oth_td_ema": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _P]),
     "oth_td_new_before": (_I, [_P, _I64, _P, _P, _P, _P]),
     "oth_td_segments": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "oth_td_segments_words": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "oth_td_ema_split": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64, _I64, _P, _P,
                               _P]),
     "oth_td_sort_pairs": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),

@@ -374,7 +374,7 @@ __device__ __forceinline__ u64 sel_nz(u64 t, u64 x) {  // t != 0 ? x : 0
         "s_nop 1\n\t"
         "v_cndmask_b32_e64 %0, 0, %4, %2\n\t"
         "v_cndmask_b32_e64 %1, 0, %5, %2"
-        : "=v"(lo), "=v"(hi), "=&s"(m)
+        : "=&v"(lo), "=&v"(hi), "=&s"(m)  // early-clobber: lo is written before x's high half is read
         : "v"(t), "v"((u32)x), "v"((u32)(x >> 32)));
     return ((u64)hi << 32) | lo;
 }
@@ -430,6 +430,29 @@ __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;
     analyse<ORDER>(P, O, s);
     return s.legal;
+}
+
+// Legal moves only, the reach folded in direction by direction (round 5, A/B
+// for the 1-ply policies' child evaluation: analyse keeps all eight run sets
+// live until the reach; here each direction's run set dies at its shift).
+// Same result as moves().
+__device__ __forceinline__ u64 moves_lean(u64 P, u64 O) {
+    const u64 Oi = and2(O, INNER_FILES);
+    u64 m = sh<1, true>(east_run(P, Oi));
+    m = or2(m, sh<1, false>(rev64(east_run(rev64(P), rev64(Oi)))));
+    {
+        const PairProp v = pair_prop<8>(O);
+        m = or3(m, sh<8, true>(and2(ks<8, true>(P, v), O)), sh<8, false>(and2(ks<8, false>(P, v), O)));
+    }
+    {
+        const PairProp d = pair_prop<9>(Oi);
+        m = or3(m, sh<9, true>(and2(ks<9, true>(P, d), O)), sh<9, false>(and2(ks<9, false>(P, d), O)));
+    }
+    {
+        const PairProp d = pair_prop<7>(Oi);
+        m = or3(m, sh<7, true>(and2(ks<7, true>(P, d), O)), sh<7, false>(and2(ks<7, false>(P, d), O)));
+    }
+    return bitop3<0x04>(P, m, O);  // ~P & m & ~O
 }
 
 // Board.puttables(Empty) (board.py:46-52 with piece = Empty, hostile(Empty) =

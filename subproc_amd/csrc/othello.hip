@@ -137,10 +137,17 @@ __device__ __forceinline__ const int* child_row(u64 P, u64 O, const int* w_tab) 
     if (POLICY != OTH_POLICY_EVAL) return w_tab;
     return w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
 }
+#ifndef OTH_CHILD_LEAN  // A/B builds: the greedy child's mobility by moves_lean (bitboard.hpp)
+#define OTH_CHILD_LEAN 0
+#endif
 template <int POLICY>
 __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* row) {
     place(P, O, flips_rays(sq, s, rays));
+#if OTH_CHILD_LEAN
+    if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves_lean(O, P)) << 6) | sq;
+#else
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O, P)) << 6) | sq;
+#endif
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
@@ -158,7 +165,7 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
     const RunSets s = run_sets(pos);
     const int* row = child_row<POLICY>(P, O, w_tab);
     while (legal) {
-        const u32 sq = (u32)__ffsll((unsigned long long)legal) - 1u;
+        const u32 sq = (u32)__builtin_ctzll(legal);  // legal != 0
         legal &= legal - 1;
         best = min(best, child_key<POLICY>(P, O, s, sq, rays, row));
     }
@@ -274,7 +281,7 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
             if (kHold) enter(p);
         }
         if (!kHold) enter(p);
-        const u32 sq = (u32)__ffsll((unsigned long long)m) - 1u;
+        const u32 sq = (u32)__builtin_ctzll(m);  // m != 0 here: no zero case (__ffsll's select)
         m &= m - 1;
         atomicMin(&cw.best[p], child_key<POLICY>(Pp, Op, ps, sq, rays, row));
     }
@@ -557,7 +564,7 @@ struct RolloutArgs {
 // next batch; once 64 games are parked they are played out as a batch of their
 // own, and a wave that finds the queue empty plays out what it has parked.
 #ifndef OTH_HANDOFF
-#define OTH_HANDOFF 0
+#define OTH_HANDOFF 1
 #endif
 constexpr u32 kHandoffK = 16;                       // the default K (env OTH_HANDOFF_K)
 constexpr u32 kHandoffKMax = 16;                    // the pool's capacity allows K up to this

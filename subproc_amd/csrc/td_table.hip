@@ -93,16 +93,13 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
 #ifndef OTH_SORT_ROUNDS
 #define OTH_SORT_ROUNDS 16
 #endif
-#ifndef OTH_SORT_DIGIT_WALK
-#define OTH_SORT_DIGIT_WALK 0
+#ifndef OTH_SORT_GROUP
+#define OTH_SORT_GROUP 16
 #endif
-#ifndef OTH_SORT_NEAR
-#define OTH_SORT_NEAR 4
-#endif
-#ifndef OTH_SORT_WAITFAR
-#define OTH_SORT_WAITFAR 32
-#endif
-constexpr int kSortNear = OTH_SORT_NEAR, kSortWaitFar = OTH_SORT_WAITFAR;
+constexpr int kSortGroup = OTH_SORT_GROUP;  // tiles per look-back group
+// a look-back poll that has not seen its word after this many polls gives up
+// (and sets a bit of the sort's error word) rather than hang the GPU
+constexpr uint32_t kSortSpinMax = 1u << 18;
 // diagnostic builds only (wrong output, for timing the parts): no look-back;
 // the tile written back in place, unscattered
 #ifndef OTH_SORT_DIAG_NOLOOK
@@ -110,7 +107,7 @@ constexpr int kSortNear = OTH_SORT_NEAR, kSortWaitFar = OTH_SORT_WAITFAR;
 #endif
 #ifndef OTH_SORT_DIAG_LINEAR
 #define OTH_SORT_DIAG_LINEAR 0
-#endif  // look-back window (tiles per digit in flight)
+#endif
 constexpr int kSortDigitBits = OTH_SORT_DIGIT;
 constexpr int kSortDigits = 1 << kSortDigitBits;
 constexpr int kSortWaves = OTH_SORT_WAVES;
@@ -206,8 +203,8 @@ __global__ __launch_bounds__(kSortHistBlock) void sort_hist_kernel(const uint64_
 template <bool UNPACK>
 __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int64_t n, int shift, uint32_t dmask, uint32_t tag,
-    const unsigned long long* __restrict__ hist, unsigned* __restrict__ status, size_t vec_off,
-    unsigned* __restrict__ ticket, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
+    const unsigned long long* __restrict__ hist, unsigned* __restrict__ status, size_t vec_off, size_t gsum_off,
+    int64_t ngroups, unsigned* __restrict__ ticket, unsigned* __restrict__ err, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
     double* __restrict__ vals_out) {
     __shared__ uint64_t stage[kSortTile];
     __shared__ uint32_t wcnt[kSortWaves][kSortDigits];  // a wave's running counts, then its prefix over waves
@@ -215,7 +212,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
     __shared__ long long gbase[kSortDigits];            // output index of the tile's slot 0, per digit
     __shared__ uint32_t wsum[kSortWaves];
     __shared__ unsigned long long hsum[kSortWaves];
-    __shared__ uint32_t tile_s, look_k;
+    __shared__ uint32_t tile_s, look_k, look_inc;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     if (tid == 0) tile_s = atomicAdd(ticket, 1u);
     for (int e = tid; e < kSortWaves * kSortDigits; e += kSortThreads) (&wcnt[0][0])[e] = 0;
@@ -229,7 +226,9 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         const int64_t i = wbase + k * 64 + lane;
         v[k] = i < n ? in[i] : 0ull;
     }
-    volatile uint32_t* wc = wcnt[wave];
+    // (the counters read and bumped by wavefront-scope atomics on the LDS
+    // array itself: a volatile pointer to them made hipcc use FLAT accesses
+    // with a vmcnt wait each)
     uint32_t rank[kSortRounds];
 #pragma unroll
     for (int k = 0; k < kSortRounds; k++) {
@@ -243,10 +242,11 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
             peers &= bit ? m : ~m;
         }
         const uint32_t below = lanes_below(peers);
-        const uint32_t old = valid ? wc[d] : 0u;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (valid && below == 0) wc[d] = old + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t old =
+            valid ? __hip_atomic_load(&wcnt[wave][d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0u;
+        if (valid && below == 0)
+            __hip_atomic_store(&wcnt[wave][d], old + (uint32_t)__popcll(peers), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
         rank[k] = old + below;
     }
     __syncthreads();
@@ -290,74 +290,40 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         tpre += wsum[w];
         hpre += hsum[w];
     }
-#if OTH_SORT_DIGIT_WALK
-    // (A/B) each digit's chain walked by its own thread, the status words laid
-    // out [digit][tile] so that a walk reads consecutive words
-    unsigned long long acc[kSortDigitsPerThread];
-    {
-        uint64_t* dw = reinterpret_cast<uint64_t*>(status + vec_off);
-        const int64_t nt = gridDim.x;
-        const uint64_t tagw = (uint64_t)tag << 56;
-        bool open[kSortDigitsPerThread];
-        int64_t tl[kSortDigitsPerThread];
+    // publish the tile's counts, look back over the tiles before it, publish
+    // the inclusive counts.
+    // * One 64-bit word per (tile, digit): flag (1 = the tile's own count,
+    //   2 = inclusive of every tile before it) << 62 | pass tag << 56 | count,
+    //   self-validating, so no fence orders anything (a reader takes a word
+    //   only once its tag is this pass's and its flag is set; on gfx950 a
+    //   release fence per tile would write back the XCD's whole L2, the
+    //   sort's scattered output included: 3-5 ms per sort, measured).
+    // * One hint word per tile (tag << 2 | the same flag), stored after the
+    //   tile's words: wave 0 polls the hints of up to 64 tiles at once.
+    // * Group sums: the tiles of a group of kSortGroup add their counts into
+    //   the group's sum (returning atomics, so the adds are done before the
+    //   group's done-counter is bumped).  A block sums tile by tile only within
+    //   its own group; before it, a whole group at a time (one vector), back to
+    //   the nearest group whose last tile is inclusive.  The first wave of
+    //   blocks of a pass starts before any tile is inclusive: tile by tile,
+    //   the last of them would each read hundreds of tiles' counts (1.2 GB of
+    //   status reads per pass, measured 2.34 ms per sort against 0.89 without
+    //   any look-back).
+    {  // the tile's digit offsets first: the LDS staging below needs no look-back
+        uint32_t tp = tpre;
 #pragma unroll
         for (int j = 0; j < kSortDigitsPerThread; j++) {
-            const int d = tid * kSortDigitsPerThread + j;
-            __hip_atomic_store(dw + d * nt + tile, ((tile ? 1ull : 2ull) << 62) | tagw | tot[j], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            acc[j] = 0;
-            open[j] = tile > 0;
-            tl[j] = tile - 1;
-        }
-        for (;;) {
-            bool any = false;
-            uint64_t x[kSortDigitsPerThread];
-#pragma unroll
-            for (int j = 0; j < kSortDigitsPerThread; j++) {
-                const int d = tid * kSortDigitsPerThread + j;
-                x[j] = open[j] ? __hip_atomic_load(dw + d * nt + tl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : 0ull;
-            }
-#pragma unroll
-            for (int j = 0; j < kSortDigitsPerThread; j++) {
-                if (!open[j]) continue;
-                if (((x[j] >> 56) & 63u) == tag && (x[j] >> 62) != 0) {
-                    acc[j] += x[j] & ((1ull << 56) - 1);
-                    if ((x[j] >> 62) == 2) open[j] = false;
-                    else tl[j]--;
-                }
-                any |= open[j];
-            }
-            if (!any) break;
-        }
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++) {
-            const int d = tid * kSortDigitsPerThread + j;
-            if (tile)
-                __hip_atomic_store(dw + d * nt + tile, (2ull << 62) | tagw | (acc[j] + tot[j]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            blk_off[tid * kSortDigitsPerThread + j] = tp;
+            tp += tot[j];
         }
     }
-#else
-    // publish the tile's counts, look back over the tiles before it, publish
-    // the inclusive counts.  Status: one 64-bit word per (tile, digit),
-    //   flag (1 = the tile's own count, 2 = inclusive of every tile before it)
-    //   << 62 | pass tag << 56 | count,
-    // self-validating, so no fence orders anything: a reader takes a word only
-    // once its tag is this pass's and its flag is set.  And one hint word per
-    // tile (tag << 2 | the same flag), stored after the tile's words, which
-    // wave 0 polls for the 64 tiles before it at once to find how far back the
-    // nearest inclusive tile lies; every thread then loads its digits' words of
-    // those tiles together, re-polling a word not yet visible, and stops at its
-    // first inclusive one.  (Round 5's first version walked each digit's chain
-    // on its own thread, tile by tile: 1.4 ms of a 2.3 ms sort.  A flag per
-    // tile over plain count vectors needs a release fence per tile, which on
-    // gfx950 writes back the XCD's whole L2, the sort's scattered output
-    // included: 3-5 ms.)
     uint32_t* hint = status;
     uint64_t* word = reinterpret_cast<uint64_t*>(status + vec_off);
+    uint32_t* gsum = status + gsum_off;  // this pass's group sums (groups x digits), then done counters
+    uint32_t* gdone = gsum + (size_t)ngroups * kSortDigits;
     uint64_t* mine = word + (size_t)tile * kSortDigits;
     const uint64_t tagw = (uint64_t)tag << 56;
+    const int64_t grp = tile / kSortGroup, first_in_grp = grp * kSortGroup;
 #pragma unroll
     for (int j = 0; j < kSortDigitsPerThread; j++)
         __hip_atomic_store(mine + tid * kSortDigitsPerThread + j, ((tile ? 1ull : 2ull) << 62) | tagw | tot[j],
@@ -365,6 +331,25 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
     __syncthreads();
     if (tid == 0)
         __hip_atomic_store(hint + tile, (tag << 2) | (tile ? 1u : 2u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {
+        uint32_t dep = 0;
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++)
+            if (tot[j])
+                dep |= __hip_atomic_fetch_add(gsum + (size_t)grp * kSortDigits + tid * kSortDigitsPerThread + j, tot[j],
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(dep) : "memory");  // every add of this thread done
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(gdone + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the tile in digit order in LDS, while the tiles before it publish
+#pragma unroll
+    for (int k = 0; k < kSortRounds; k++) {
+        if (wbase + k * 64 + lane < n) {
+            const uint32_t d = sort_digit(v[k], shift, dmask);
+            stage[blk_off[d] + wcnt[wave][d] + rank[k]] = v[k];
+        }
+    }
     unsigned long long acc[kSortDigitsPerThread];
     bool open[kSortDigitsPerThread];
 #pragma unroll
@@ -372,61 +357,124 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         acc[j] = 0;
         open[j] = tile > 0 && !OTH_SORT_DIAG_NOLOOK;
     }
-    int64_t hi_t = tile - 1;  // the nearest predecessor not yet summed
-    while (hi_t >= 0 && !OTH_SORT_DIAG_NOLOOK) {
+    // a tile's words: summed (own or inclusive); need_inc: poll until inclusive
+    auto take_tile = [&](int64_t t, bool need_inc) {
+        const uint64_t* tw = word + (size_t)t * kSortDigits + tid * kSortDigitsPerThread;
+        uint64_t x[kSortDigitsPerThread];
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++)
+            x[j] = open[j] ? __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+        for (int j = 0; j < kSortDigitsPerThread; j++) {
+            if (!open[j]) continue;
+            // (a hint may be visible before the words it follows: poll them)
+            for (uint32_t spin = 0;
+                 ((x[j] >> 56) & 63u) != tag || (x[j] >> 62) == 0 || (need_inc && (x[j] >> 62) != 2); spin++) {
+                if (spin > kSortSpinMax) {  // never expected: report, do not hang the GPU
+                    atomicOr(err, 1u);
+                    break;
+                }
+                x[j] = __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            acc[j] += x[j] & ((1ull << 56) - 1);
+            if ((x[j] >> 62) == 2) open[j] = false;
+        }
+    };
+    // phase A: the tiles of this block's group before it, up to 64 hints a poll
+    int64_t hi_t = tile - 1;
+    bool done = tile == 0 || OTH_SORT_DIAG_NOLOOK;
+    while (!done && hi_t >= first_in_grp) {
         if (wave == 0) {
-            uint32_t k = 0, polls = 0;
-            for (;; polls++) {
+            uint32_t k = 0;
+            for (uint32_t spin = 0;; spin++) {
+                if (spin > kSortSpinMax) {
+                    if (lane == 0) atomicOr(err, 2u);
+                    k = (uint32_t)(hi_t - first_in_grp + 1);
+                    break;
+                }
                 const int64_t t = hi_t - lane;
                 const uint32_t f =
-                    t >= 0 ? __hip_atomic_load(hint + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                    t >= first_in_grp ? __hip_atomic_load(hint + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
                 const bool ready = (f >> 2) == tag && (f & 3u) != 0;
                 const uint64_t mr = __ballot(ready), mi = __ballot(ready && (f & 3u) == 2u);
                 const uint32_t first_gap = mr == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mr);
                 const uint32_t near_inc = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
-                // an inclusive tile within kSortNear: its own counts and the
-                // tiles' between; farther back, wait up to kSortWaitFar polls
-                // for the inclusive front to come closer (the first wave of
-                // blocks would each read hundreds of tiles' counts), then sum
-                // what is published
-                const bool patient = polls < (uint32_t)kSortWaitFar;
-                if (near_inc < first_gap && (near_inc < (uint32_t)kSortNear || !patient)) {
+                if (near_inc < first_gap) {  // own counts, then an inclusive tile
                     k = near_inc + 1;
                     break;
                 }
-                if (first_gap > 0 && !patient) {  // own counts only: sum them, look further back
-                    k = first_gap;
+                if (first_gap > 0 && (first_gap < 64u || hi_t - 63 < first_in_grp)) {
+                    k = first_gap;  // own counts (to the group's first tile, or a tile not yet published)
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(1);  // the nearest tile has not published yet
             }
             if (lane == 0) look_k = k;
         }
         __syncthreads();
         const int64_t k = look_k;
-        for (int64_t i = 0; i < k; i++) {
-            const uint64_t* tw = word + (size_t)(hi_t - i) * kSortDigits + tid * kSortDigitsPerThread;
-            uint64_t x[kSortDigitsPerThread];
-#pragma unroll
-            for (int j = 0; j < kSortDigitsPerThread; j++)
-                x[j] = open[j] ? __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-#pragma unroll
-            for (int j = 0; j < kSortDigitsPerThread; j++) {
-                if (!open[j]) continue;
-                // (the hint may be visible before the word: poll it.  A word
-                // still holding the tile's own count where the hint said
-                // inclusive is summed as such, and the walk goes on.)
-                while (((x[j] >> 56) & 63u) != tag || (x[j] >> 62) == 0)
-                    x[j] = __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                acc[j] += x[j] & ((1ull << 56) - 1);
-                if ((x[j] >> 62) == 2) open[j] = false;
-            }
-        }
+        for (int64_t i = 0; i < k; i++) take_tile(hi_t - i, false);
         hi_t -= k;
         bool any = false;
 #pragma unroll
         for (int j = 0; j < kSortDigitsPerThread; j++) any |= open[j];
-        if (!__syncthreads_or(any)) break;  // every digit reached an inclusive count
+        done = !__syncthreads_or(any);  // every digit reached an inclusive count
+    }
+    // phase B: whole groups before this block's, up to 64 a poll: complete
+    // group sums back to the nearest group whose last tile is inclusive
+    int64_t hi_g = grp - 1;
+    while (!done) {
+        if (wave == 0) {
+            uint32_t k = 0, inc = 0;
+            for (uint32_t spin = 0;; spin++) {
+                if (spin > kSortSpinMax || hi_g < 0) {
+                    if (lane == 0) atomicOr(err, hi_g < 0 ? 8u : 4u);
+                    k = (uint32_t)max<int64_t>(hi_g + 1, 0);
+                    inc = 0;
+                    break;
+                }
+                const int64_t g = hi_g - lane;
+                uint32_t fd = 0, fh = 0;
+                if (g >= 0) {
+                    fd = __hip_atomic_load(gdone + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    fh = __hip_atomic_load(hint + (g + 1) * kSortGroup - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                const uint64_t mr = __ballot(g >= 0 && fd == (uint32_t)kSortGroup);
+                const uint64_t mi = __ballot(g >= 0 && fh == ((tag << 2) | 2u));
+                const uint32_t first_gap = mr == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mr);
+                const uint32_t near_inc = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
+                if (near_inc <= first_gap && near_inc < 64u) {  // complete groups, then an inclusive tile
+                    k = near_inc;
+                    inc = 1;
+                    break;
+                }
+                if (first_gap > 0) {  // complete groups only: sum them, look further back
+                    k = first_gap;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) {
+                look_k = k;
+                look_inc = inc;
+            }
+        }
+        __syncthreads();
+        const int64_t k = look_k;
+        const bool inc = look_inc;
+        for (int64_t i = 0; i < k; i++) {
+            const uint32_t* gv = gsum + (size_t)(hi_g - i) * kSortDigits + tid * kSortDigitsPerThread;
+#pragma unroll
+            for (int j = 0; j < kSortDigitsPerThread; j++)
+                if (open[j]) acc[j] += __hip_atomic_load(gv + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        hi_g -= k;
+        if (hi_g < 0) done = true;  // (only after a reported error)
+        if (inc) {
+            take_tile((hi_g + 1) * kSortGroup - 1, true);  // the inclusive last tile of group hi_g
+            done = true;
+        }
+        __syncthreads();  // look_k / look_inc read before wave 0 writes them again
     }
     if (tile) {
 #pragma unroll
@@ -436,23 +484,12 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         __syncthreads();
         if (tid == 0) __hip_atomic_store(hint + tile, (tag << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
 #pragma unroll
     for (int j = 0; j < kSortDigitsPerThread; j++) {
         const int d = tid * kSortDigitsPerThread + j;
-        blk_off[d] = tpre;
         gbase[d] = (long long)(hpre + acc[j]) - (long long)tpre;
         tpre += tot[j];
         hpre += hcnt[j];
-    }
-    __syncthreads();
-    // the tile in digit order in LDS
-#pragma unroll
-    for (int k = 0; k < kSortRounds; k++) {
-        if (wbase + k * 64 + lane < n) {
-            const uint32_t d = sort_digit(v[k], shift, dmask);
-            stage[blk_off[d] + wcnt[wave][d] + rank[k]] = v[k];
-        }
     }
     __syncthreads();
     const int nv = (int)min<int64_t>(kSortTile, n - t0);
@@ -474,7 +511,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
 struct SortPlan {
     int passes;
     int64_t tiles;
-    size_t words_off, hist_off, ticket_off, status_off, vec_off, bytes;
+    int64_t groups;
+    size_t words_off, hist_off, ticket_off, status_off, vec_off, gsum_off, bytes;
 };
 inline SortPlan sort_plan(int64_t n, int bits) {
     SortPlan p;
@@ -484,12 +522,16 @@ inline SortPlan sort_plan(int64_t n, int bits) {
     p.words_off = 0;
     p.hist_off = al((size_t)n * sizeof(uint64_t));
     p.ticket_off = al(p.hist_off + (size_t)p.passes * kSortDigits * sizeof(unsigned long long));
-    p.status_off = al(p.ticket_off + (size_t)p.passes * sizeof(unsigned));
+    p.status_off = al(p.ticket_off + (size_t)(kSortMaxPasses + 1) * sizeof(unsigned));  // tickets, error word
     // status: the tiles' hint words, then their (tile, digit) words (vec_off:
     // in 32-bit units, even)
     const size_t tiles = (size_t)std::max<int64_t>(p.tiles, 1);
     p.vec_off = (tiles + 63) / 64 * 64;
-    p.bytes = al(p.status_off + (p.vec_off + tiles * 2 * kSortDigits) * sizeof(uint32_t));
+    // then per pass the group sums and the groups' done counters (32-bit units)
+    p.groups = (int64_t)((tiles + kSortGroup - 1) / kSortGroup);
+    p.gsum_off = p.vec_off + tiles * 2 * kSortDigits;
+    p.bytes = al(p.status_off +
+                 (p.gsum_off + (size_t)p.passes * ((size_t)p.groups * (kSortDigits + 1) + 64)) * sizeof(uint32_t));
     return p;
 }
 // the sort of n words by bits [0, bits): into out (keys NULL) or unpacked into
@@ -524,11 +566,13 @@ hipError_t sort_words(const uint64_t* in, uint64_t* out, int64_t n, int bits, co
         if (keys && last)
             sort_pass_kernel<true><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
                 src, nullptr, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
-                p.vec_off, ticket + q, lam_pow, keys, vals);
+                p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
+                ticket + kSortMaxPasses, lam_pow, keys, vals);
         else
             sort_pass_kernel<false><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
                 src, dst, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
-                p.vec_off, ticket + q, nullptr, nullptr, nullptr);
+                p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
+                ticket + kSortMaxPasses, nullptr, nullptr, nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         src = dst;
     }
@@ -881,44 +925,59 @@ constexpr int kSegWavesPerBlock = kSegBlock / 64;
 // leaves the wave's two counts, the write pass (after their scans) places
 // both in order.  (The long keys by atomic appends instead: 25k appends to
 // one counter cost the write pass 83 -> 368 us.)
-template <bool WRITE>
+// WORDS (oth_td_segments_words, round 5): the input is the key-sorted packed
+// words themselves, each read as its key (the low OTH_TD_KEY_BITS), and the
+// write pass also writes every update's value (oth_td_unpack's rule), so the
+// sorted stream needs no separate unpack into a keys array and a values array.
+template <bool WRITE, bool WORDS = false>
 __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __restrict__ keys, int64_t n,
                                                            int64_t* __restrict__ wave_cnt,
                                                            int64_t* __restrict__ wave_lcnt,
                                                            int64_t* __restrict__ seg_off,
                                                            int64_t* __restrict__ ukeys, int64_t long_min,
-                                                           int64_t* __restrict__ long_idx) {
+                                                           int64_t* __restrict__ long_idx,
+                                                           const double* __restrict__ lam_pow = nullptr,
+                                                           double* __restrict__ values = nullptr) {
     __shared__ int64_t stage[kSegWavesPerBlock][kSegWaveKeys + 64];
+    constexpr int64_t kKeyMask = (1ll << OTH_TD_KEY_BITS) - 1;
+    auto key_of = [](int64_t x) { return WORDS ? (x & kKeyMask) : x; };
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
     const int64_t base = w * kSegWaveKeys;
     if (base >= n) return;  // wave-uniform
     // every round's key loaded before the first is used (17 loads in flight)
     int64_t k[kSegRounds];
+    uint32_t payload[kSegRounds];  // WORDS, WRITE: the word's top 21 bits
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
-        k[r] = i < n ? keys[i] : 0;
+        const int64_t x = i < n ? keys[i] : 0;
+        k[r] = key_of(x);
+        payload[r] = (uint32_t)((uint64_t)x >> OTH_TD_PACK_TURN_SHIFT);
     }
     int64_t* mine = stage[threadIdx.x >> 6];
     {
         const int64_t i = base + kSegWaveKeys + lane;
-        mine[kSegWaveKeys + lane] = i < n ? keys[i] : -1;  // (keys are >= 0)
+        mine[kSegWaveKeys + lane] = i < n ? key_of(keys[i]) : -1;  // (keys are >= 0)
     }
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) mine[r * 64 + lane] = k[r];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    int64_t prev_last = base > 0 ? keys[base - 1] : 0;
+    int64_t prev_last = base > 0 ? key_of(keys[base - 1]) : 0;
     int64_t pos = WRITE ? wave_cnt[w] : 0, lpos = WRITE ? wave_lcnt[w] : 0;  // after the scans: the wave's firsts
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
+        if (WORDS && WRITE && i < n) {
+            const int vs = (int)(payload[r] >> (OTH_TD_PACK_VALUE_SHIFT - OTH_TD_PACK_TURN_SHIFT)) - 64;
+            values[i] = (double)vs * lam_pow[payload[r] & 0x1fffu];
+        }
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
         const bool start = i < n && (i == 0 || k[r] != before);
         const int64_t e = i + long_min - 1, off = e - base;
-        const bool lng = start && e < n && (off < kSegWaveKeys + 64 ? mine[off] == k[r] : keys[e] == k[r]);
+        const bool lng = start && e < n && (off < kSegWaveKeys + 64 ? mine[off] == k[r] : key_of(keys[e]) == k[r]);
         const uint64_t m = __ballot(start), ml = __ballot(lng);
         if (WRITE && start) {
             const int64_t at =
@@ -938,8 +997,6 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         wave_lcnt[w] = lpos;
     }
 }
-// the exclusive running count of is_new (oth_td_new_before), the same two
-// passes: per wave a count, then, after the scan, every position's count
 template <bool WRITE>
 __global__ __launch_bounds__(kSegBlock) void td_count_kernel(const uint8_t* __restrict__ flags, int64_t n,
                                                              int64_t* __restrict__ wave_cnt,
@@ -1136,8 +1193,11 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 
-int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
-                    int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream) {
+}  // extern "C"
+namespace {
+template <bool WORDS>
+int td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys, int64_t* long_idx,
+                int64_t* counts, const double* lam_pow, double* values, void* temp, size_t* temp_bytes, void* stream) {
     if (n < 0 || long_min < 1 || !temp_bytes) return OTH_EINVAL;
     const int64_t n_waves = (n + kSegWaveKeys - 1) / kSegWaveKeys, slots = n_waves > 0 ? n_waves : 1;
     const size_t scan_bytes = seg_scan_bytes(n_waves);
@@ -1148,6 +1208,7 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
         return OTH_OK;
     }
     if (!seg_off || !counts || (n > 0 && (!keys || !ukeys || !long_idx)) || *temp_bytes < need) return OTH_EINVAL;
+    if (WORDS && n > 0 && (!lam_pow || !values)) return OTH_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     int64_t* wave_cnt = static_cast<int64_t*>(temp);
     int64_t* wave_off = wave_cnt + slots;
@@ -1156,16 +1217,31 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
     void* scan_temp = static_cast<char*>(temp) + head;
     const unsigned blocks = (unsigned)((n_waves + kSegWavesPerBlock - 1) / kSegWavesPerBlock);
     if (n > 0)
-        td_seg_kernel<false><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, wave_lcnt, seg_off, ukeys, long_min,
-                                                          long_idx);
+        td_seg_kernel<false, WORDS><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_cnt, wave_lcnt, seg_off, ukeys,
+                                                                  long_min, long_idx);
     hipError_t e = seg_scan(wave_cnt, wave_off, n_waves, n, seg_off, counts, scan_temp, scan_bytes, st);
     if (e == hipSuccess) e = seg_scan(wave_lcnt, wave_loff, n_waves, n, nullptr, counts + 1, scan_temp, scan_bytes, st);
     if (e != hipSuccess) return -(int)e;
     if (n > 0)
-        td_seg_kernel<true><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_off, wave_loff, seg_off, ukeys, long_min,
-                                                         long_idx);
+        td_seg_kernel<true, WORDS><<<blocks, kSegBlock, 0, st>>>(keys, n, wave_off, wave_loff, seg_off, ukeys,
+                                                                 long_min, long_idx, lam_pow, values);
     e = hipGetLastError();
     return e == hipSuccess ? OTH_OK : -(int)e;
+}
+}  // namespace
+extern "C" {
+
+int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
+                    int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream) {
+    return td_segments<false>(keys, n, long_min, seg_off, ukeys, long_idx, counts, nullptr, nullptr, temp,
+                              temp_bytes, stream);
+}
+
+int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t n, int64_t long_min, int64_t* seg_off,
+                          int64_t* ukeys, int64_t* long_idx, int64_t* counts, double* values, void* temp,
+                          size_t* temp_bytes, void* stream) {
+    return td_segments<true>(reinterpret_cast<const int64_t*>(words), n, long_min, seg_off, ukeys, long_idx, counts,
+                             lam_pow, values, temp, temp_bytes, stream);
 }
 
 int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,

@@ -155,22 +155,25 @@ class StateMap:
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            # the update stream as packed words (key | value_side | turn_left), a
-            # keys-only sort of the words by their key bits (half the bytes of
-            # sorting (key, value) pairs), then keys and values back out
+            # the update stream as packed words (key | value_side | turn_left):
+            # half the bytes of (key, value) pairs through the sort
             words = torch.empty(total, dtype=torch.int64, device=self.device)
             check(lib.oth_td_updates_packed(pos_boards.contiguous().data_ptr(),
                                             None if row_off is None else row_off.contiguous().data_ptr(),
                                             plies.contiguous().data_ptr(), base.data_ptr(), words.data_ptr(), n,
                                             stream), "oth_td_updates_packed")
-            # the build's radix sort by key bits, its last pass writing the keys
-            # and values (oth_td_sort_unpack: the sort and the unpack in one)
-            sk = torch.empty(total, dtype=torch.int64, device=self.device)
-            sv = torch.empty(total, dtype=torch.float64, device=self.device)
-            _with_scratch(lib.oth_td_sort_unpack, (words.data_ptr(), self._lam_pow.data_ptr(), sk.data_ptr(),
-                                                   sv.data_ptr(), total), stream, self.device, "oth_td_sort_unpack")
+            # a keys-only sort of the words by their key bits (the payload rides
+            # along), then the segments straight from the sorted words, which
+            # also writes each update's value (oth_td_segments_words: no
+            # separate unpack into a keys array and a values array)
+            sorted_words = torch.empty_like(words)
+            _with_scratch(lib.oth_td_sort_packed, (words.data_ptr(), sorted_words.data_ptr(), total), stream,
+                          self.device, "oth_td_sort_packed")
             del words
-        self._apply_sorted(sk, sv)
+            sv = torch.empty(total, dtype=torch.float64, device=self.device)
+            segs = self._segments(sorted_words, sv)
+            del sorted_words
+        self._apply_segments(sv, *segs)
         return total
 
     def update_from_records(self, books):
@@ -220,21 +223,40 @@ class StateMap:
     def _apply_sorted(self, sk, sv):
         """The key-sorted update stream (equal keys in stream order) into the
         table: each key's EMA in stream order, then the merge."""
+        with torch.cuda.device(self.device):
+            segs = self._segments(sk, None)
+        self._apply_segments(sv, *segs)
+
+    def _segments(self, sorted_in, values):
+        """The sorted stream's segments in one pass pair and one host sync:
+        from keys (oth_td_segments), or (values given) from the sorted packed
+        words, the values written as a side effect (oth_td_segments_words).
+        Returns (ukeys, seg_off, long_idx)."""
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        n = sorted_in.numel()
+        seg_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        ukeys = torch.empty(n, dtype=torch.int64, device=self.device)
+        long_idx = torch.empty(n, dtype=torch.int64, device=self.device)
+        cnt = torch.empty(2, dtype=torch.int64, device=self.device)
+        if values is None:
+            _with_scratch(lib.oth_td_segments, (sorted_in.data_ptr(), n, LONG_MIN, seg_off.data_ptr(),
+                                                ukeys.data_ptr(), long_idx.data_ptr(), cnt.data_ptr()), stream,
+                          self.device, "oth_td_segments")
+        else:
+            _with_scratch(lib.oth_td_segments_words, (sorted_in.data_ptr(), self._lam_pow.data_ptr(), n, LONG_MIN,
+                                                      seg_off.data_ptr(), ukeys.data_ptr(), long_idx.data_ptr(),
+                                                      cnt.data_ptr(), values.data_ptr()), stream, self.device,
+                          "oth_td_segments_words")
+        n_upd, n_long = cnt.tolist()
+        return ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
+
+    def _apply_segments(self, sv, ukeys, seg_off, long_idx):
+        """Each key's EMA in stream order over its segment of sv, then the merge."""
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            # the stream's segments (keys, run offsets, the long ones) in one
-            # pass pair and one host sync (oth_td_segments)
-            n = sk.numel()
-            seg_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
-            ukeys = torch.empty(n, dtype=torch.int64, device=self.device)
-            long_idx = torch.empty(n, dtype=torch.int64, device=self.device)
-            cnt = torch.empty(2, dtype=torch.int64, device=self.device)
-            _with_scratch(lib.oth_td_segments, (sk.data_ptr(), n, LONG_MIN, seg_off.data_ptr(), ukeys.data_ptr(),
-                                                long_idx.data_ptr(), cnt.data_ptr()), stream, self.device,
-                          "oth_td_segments")
-            n_upd, n_long = cnt.tolist()
-            ukeys, seg_off, long_idx = ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
+            n_upd = ukeys.numel()
             is_new = None
             if len(self):
                 init = torch.empty(n_upd, dtype=torch.float64, device=self.device)

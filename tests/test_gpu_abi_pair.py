@@ -111,6 +111,41 @@ def test_td_sort_packed_stable(n, distinct):
     np.testing.assert_array_equal(out.h, w[np.argsort(k, kind="stable")])
 
 
+@pytest.mark.parametrize("n,distinct,offset", [(1, 1, 0), (4097, 7, 1), (300001, 5000, 0), (2_000_003, 1 << 20, 1),
+                                               (2_000_003, 3, 0)])
+def test_td_sort_unpack_pair(n, distinct, offset):
+    """oth_td_sort_unpack (round 5: the sort with the unpack in its last pass)
+    on both builds: the keys and values equal the stable sort of the words by
+    key bits followed by oth_td_unpack.  Payloads as oth_td_updates_packed
+    writes them (value_side + 64 in the top byte, turn_left 0..128 below);
+    offset 1: the words start 8 bytes into a device buffer (not 16-B aligned)."""
+    rng = np.random.default_rng(n + 7)
+    pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
+    pool[0], pool[-1] = 0, (1 << _lib.TD_KEY_BITS) - 1
+    k = pool[rng.integers(0, distinct, size=n)].astype(np.uint64)
+    vs = rng.integers(-64, 65, size=n).astype(np.int64)
+    tl = rng.integers(0, 129, size=n).astype(np.uint64)
+    w = (((vs + 64).astype(np.uint64)) << np.uint64(56)) | (tl << np.uint64(43)) | k
+    lam = np.array([0.9 ** j for j in range(129)], np.float64)
+    words = Buf(np.concatenate([np.zeros(offset, np.uint64), w]))
+    ko, vo, lamb = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64)), Buf(lam)
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    st = torch.cuda.current_stream().cuda_stream
+    for lib, src, ptr, s in ((cpu, HOSTP(words.h[offset:]), lambda b: HOSTP(b.h), None),
+                             (gpu, words.d.data_ptr() + 8 * offset, lambda b: b.d.data_ptr(), st)):
+        tb = ctypes.c_size_t(0)
+        assert lib.oth_td_sort_unpack(src, ptr(lamb), ptr(ko), ptr(vo), n, None, ctypes.byref(tb), s) == 0
+        temp = (torch.empty(max(tb.value, 1), dtype=torch.uint8, device=DEV) if lib is gpu
+                else np.zeros(max(tb.value, 1), np.uint8))
+        tp = temp.data_ptr() if lib is gpu else HOSTP(temp)
+        assert lib.oth_td_sort_unpack(src, ptr(lamb), ptr(ko), ptr(vo), n, tp, ctypes.byref(tb), s) == 0
+    torch.cuda.synchronize()
+    same(ko, vo)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(ko.h, k[order].astype(np.int64))
+    np.testing.assert_array_equal(vo.h, vs[order].astype(np.float64) * lam[tl[order].astype(np.int64)])
+
+
 @pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
 def test_td_sort_pairs_stable(n, distinct):
     """Keys over all OTH_TD_KEY_BITS key bits with many repeats: both builds sort
@@ -411,6 +446,36 @@ def test_td_segments_pair():
         want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
         assert nl == len(want)
         np.testing.assert_array_equal(li.h[:nl], want)
+        np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
+
+
+def test_td_segments_words_pair():
+    """oth_td_segments_words (round 5): the same runs read from key-sorted
+    packed words (payloads in the top 21 bits, which must not split a run),
+    and every word's value as oth_td_unpack gives it, on both builds."""
+    rng = np.random.default_rng(13)
+    lam = np.array([0.9 ** j for j in range(129)], np.float64)
+    for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 1023, 1024, 1025, 5000],
+                                                                          400)):
+        keys = np.repeat(np.cumsum(rng.integers(1, 1000, len(lens))).astype(np.uint64), lens)
+        n = len(keys)
+        vs = rng.integers(-64, 65, n).astype(np.int64)
+        tl = rng.integers(0, 129, n).astype(np.uint64)
+        w = ((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(43)) | keys
+        words, lamb = Buf(w), Buf(lam)
+        off, uk, li, cnt, val = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)),
+                                 Buf(np.zeros(n, np.int64)), Buf(np.zeros(2, np.int64)), Buf(np.zeros(n, np.float64)))
+        both_scratch("oth_td_segments_words", words, lamb, n, 48, off, uk, li, cnt, val)
+        same(cnt, val)
+        m, nl = (int(x) for x in cnt.h)
+        starts = np.flatnonzero(np.r_[True, keys[1:] != keys[:-1]])
+        assert m == len(starts)
+        np.testing.assert_array_equal(off.h[:m + 1], np.r_[starts, n])
+        np.testing.assert_array_equal(off.d.cpu().numpy()[:m + 1], off.h[:m + 1])
+        np.testing.assert_array_equal(uk.d.cpu().numpy()[:m], keys[starts].astype(np.int64))
+        np.testing.assert_array_equal(val.h, vs.astype(np.float64) * lam[tl.astype(np.int64)])
+        want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
+        assert nl == len(want)
         np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
 
 

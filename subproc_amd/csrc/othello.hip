@@ -191,8 +191,8 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
-#ifndef OTH_COOP_HOLD_EVAL  // A/B builds only (held, the eval kernel spills)
-#define OTH_COOP_HOLD_EVAL 0
+#ifndef OTH_COOP_HOLD_EVAL  // round 5: the eval kernel holds its parent record too (A/B: 0 rereads it)
+#define OTH_COOP_HOLD_EVAL 1
 #endif
 struct CoopWave {
     u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words; A1's bit 0, a1, carries the eval table)
@@ -258,9 +258,14 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
         if ((u32)__shfl((int)excl, (int)(p + step)) <= t0) p += step;
     const u32 k0 = t0 - (u32)__shfl((int)excl, (int)p);
     wave_sync();
-    // the current parent: its remaining squares m, its record and weight row
-    // (greedy holds the record across its children; eval, at its 128 VGPRs,
-    // rereads it per child: held, it spilled)
+    // the current parent: its remaining squares m, its record and weight row,
+    // held across its children.  Round 4's eval kernel reread the record from
+    // LDS per child (held, it spills a few per-batch values at its 128
+    // VGPRs): that reread on every child's dependency chain is what made
+    // eval on chunks 3.5% slower than round 3's surplus list, whose lanes
+    // mostly evaluated their own children (PMC: same VALU per child within
+    // 2%, round 5, profiles/r05_notes.md); held, eval runs at round 3's speed
+    // (3.810 against 3.817 ms per 1M-game launch, 3.945 rereading)
     constexpr bool kHold = POLICY != OTH_POLICY_EVAL || OTH_COOP_HOLD_EVAL;
     u64 m = 0, Pp = 0, Op = 0;
     RunSets ps = {};
@@ -607,7 +612,11 @@ constexpr size_t rec_stage_bytes(int policy, bool record) {
 #endif
 constexpr int kRandomFillOrder = OTH_RANDOM_FILL_ORDER;
 template <int POLICY, bool RECORD, bool RUNNER = false>
-__global__ __launch_bounds__(kBlock, 4) void rollout_kernel(RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
+#ifndef OTH_EVAL_WAVES_PER_SIMD  // A/B builds: the eval kernels' occupancy floor (launch bounds)
+#define OTH_EVAL_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL ? OTH_EVAL_WAVES_PER_SIMD : 4) void rollout_kernel(
+    RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
     const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long diag_iters = 0;

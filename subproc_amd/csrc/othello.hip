@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void result_kernel(const u64* __restrict__ 
 // word), plays the 64 games to terminal in lockstep -- a finished lane is
 // masked off until the whole batch is done -- and dequeues again.  The
 // hardware balances the batches; no refill code runs inside the ply loop
-// (measured cheaper than per-lane refill, DESIGN.md §Rollout scheduling).
+// (measured cheaper than per-lane refill, profiles/design_history_r01_r04.md §Rollout scheduling).
 //
 // The work word is the caller's (include/othello.h): 0 when the launch
 // starts, and 0 again when it ends.  A launch of B batches on W waves makes
@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(kBlock) void td_records_kernel(const u64* __restric
 // A key's updates number up to ~2 per game (the first plies), so long segments
 // are software-pipelined: a ring of three chunks keeps 2 * kTdChunk loads in
 // flight while the dependent multiply/add/select chain consumes the third
-// (69.5 ms -> see there for a 262,144-game batch).
+// (profiles/design_history_r01_r04.md §10: 69.5 ms for a 262,144-game batch).
 constexpr int kTdChunk = 16;
 __device__ __forceinline__ double td_step(double v, double x, double a, double oma) {
 #pragma clang fp contract(off)

@@ -15,7 +15,7 @@
 // (the gfx950 default of 8 bits a pass took 7 passes, 2.11-2.13 ms,
 // tools/diag/sort_bits.hip; 10 bits ran 3.58 ms, 11 do not fit the LDS).
 // torch.sort of the keys with a permutation is 8 passes of (key, int64 index)
-// pairs plus a gather of the values by that permutation.
+// pairs plus a gather of the values by that permutation (profiles/design_history_r01_r04.md §10).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,7 +28,7 @@
 namespace {
 
 // onesweep digit width, items per thread and block size (build knobs for A/B
-// builds only; the product build uses the defaults)
+// builds only, profiles/r05_notes.md; the product build uses the defaults)
 #ifndef OTH_SORT_BITS
 #define OTH_SORT_BITS 9
 #endif

@@ -276,8 +276,8 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
     fresh games per GPU (+ the histogram all-reduce at N>1).  Steps are issued
     round-robin on `nstreams` HIP streams, each with its own output buffers:
     a launch's last batches (the per-launch tail) then share
-    the CUs with the next step's first batches instead of idling them.  Every step still plays all of its games; nstreams=1 is
-    the serialized figure."""
+    the CUs with the next step's first batches instead of idling them.  Every
+    step still plays all of its games; nstreams=1 is the serialized figure."""
     from subproc_amd import _lib
     from subproc_amd._lib import HIST_BINS
     from subproc_amd.dist import bench_game_id0

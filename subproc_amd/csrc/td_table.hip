@@ -108,6 +108,9 @@ constexpr uint32_t kSortSpinMax = 1u << 18;
 #ifndef OTH_SORT_DIAG_LINEAR
 #define OTH_SORT_DIAG_LINEAR 0
 #endif
+#ifndef OTH_SORT_DIAG_TIME
+#define OTH_SORT_DIAG_TIME 0
+#endif
 constexpr int kSortDigitBits = OTH_SORT_DIGIT;
 constexpr int kSortDigits = 1 << kSortDigitBits;
 constexpr int kSortWaves = OTH_SORT_WAVES;
@@ -204,7 +207,7 @@ template <bool UNPACK>
 __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int64_t n, int shift, uint32_t dmask, uint32_t tag,
     const unsigned long long* __restrict__ hist, unsigned* __restrict__ status, size_t vec_off, size_t gsum_off,
-    int64_t ngroups, unsigned* __restrict__ ticket, unsigned* __restrict__ err, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
+    int64_t ngroups, unsigned* __restrict__ ticket, unsigned* __restrict__ err, size_t diag_off, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
     double* __restrict__ vals_out) {
     __shared__ uint64_t stage[kSortTile];
     __shared__ uint32_t wcnt[kSortWaves][kSortDigits];  // a wave's running counts, then its prefix over waves
@@ -218,6 +221,13 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
     for (int e = tid; e < kSortWaves * kSortDigits; e += kSortThreads) (&wcnt[0][0])[e] = 0;
     __syncthreads();
     const int64_t tile = tile_s;
+#if OTH_SORT_DIAG_TIME
+    // (diagnostic builds: s_memtime at entry, before the look-back, after it,
+    // at exit; the scratch's diag area, 4 words per tile per pass)
+    unsigned long long* const dgt =
+        reinterpret_cast<unsigned long long*>(status + diag_off) + ((size_t)(tag - 1) * gridDim.x + tile) * 4;
+    const unsigned long long dt0 = __builtin_amdgcn_s_memtime();
+#endif
     const int64_t t0 = tile * kSortTile, wbase = t0 + (int64_t)wave * (kSortRounds * 64);
     // the wave's words, every round's load in flight before the first is ranked
     uint64_t v[kSortRounds];
@@ -380,6 +390,9 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
             if ((x[j] >> 62) == 2) open[j] = false;
         }
     };
+#if OTH_SORT_DIAG_TIME
+    const unsigned long long dt1 = __builtin_amdgcn_s_memtime();
+#endif
     // phase A: the tiles of this block's group before it, up to 64 hints a poll
     int64_t hi_t = tile - 1;
     bool done = tile == 0 || OTH_SORT_DIAG_NOLOOK;
@@ -492,6 +505,9 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         hpre += hcnt[j];
     }
     __syncthreads();
+#if OTH_SORT_DIAG_TIME
+    const unsigned long long dt2 = __builtin_amdgcn_s_memtime();
+#endif
     const int nv = (int)min<int64_t>(kSortTile, n - t0);
 #pragma unroll 4
     for (int s = tid; s < nv; s += kSortThreads) {
@@ -505,6 +521,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
             out[pos] = w;
         }
     }
+#if OTH_SORT_DIAG_TIME
+    __syncthreads();
+    if (tid == 0) {
+        dgt[0] = dt0;
+        dgt[1] = dt1;
+        dgt[2] = dt2;
+        dgt[3] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // scratch: [ping-pong words (n) | histograms | tickets | status (tiles x digits)]
@@ -512,7 +537,7 @@ struct SortPlan {
     int passes;
     int64_t tiles;
     int64_t groups;
-    size_t words_off, hist_off, ticket_off, status_off, vec_off, gsum_off, bytes;
+    size_t words_off, hist_off, ticket_off, status_off, vec_off, gsum_off, diag_off, bytes;
 };
 inline SortPlan sort_plan(int64_t n, int bits) {
     SortPlan p;
@@ -530,8 +555,10 @@ inline SortPlan sort_plan(int64_t n, int bits) {
     // then per pass the group sums and the groups' done counters (32-bit units)
     p.groups = (int64_t)((tiles + kSortGroup - 1) / kSortGroup);
     p.gsum_off = p.vec_off + tiles * 2 * kSortDigits;
-    p.bytes = al(p.status_off +
-                 (p.gsum_off + (size_t)p.passes * ((size_t)p.groups * (kSortDigits + 1) + 64)) * sizeof(uint32_t));
+    // (diagnostic builds: then 4 timestamps per tile per pass, 64-bit aligned)
+    p.diag_off = (p.gsum_off + (size_t)p.passes * ((size_t)p.groups * (kSortDigits + 1) + 64) + 1) / 2 * 2;
+    p.bytes = al(p.status_off + p.diag_off * sizeof(uint32_t) +
+                 (OTH_SORT_DIAG_TIME ? (size_t)p.passes * tiles * 4 * sizeof(uint64_t) : 0));
     return p;
 }
 // the sort of n words by bits [0, bits): into out (keys NULL) or unpacked into
@@ -567,12 +594,12 @@ hipError_t sort_words(const uint64_t* in, uint64_t* out, int64_t n, int bits, co
             sort_pass_kernel<true><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
                 src, nullptr, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
                 p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
-                ticket + kSortMaxPasses, lam_pow, keys, vals);
+                ticket + kSortMaxPasses, p.diag_off, lam_pow, keys, vals);
         else
             sort_pass_kernel<false><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
                 src, dst, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
                 p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
-                ticket + kSortMaxPasses, nullptr, nullptr, nullptr);
+                ticket + kSortMaxPasses, p.diag_off, nullptr, nullptr, nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         src = dst;
     }

@@ -173,3 +173,41 @@ def test_rollout_runner_fixtures(name):
                                     P(WORK), 4, None) == E
     assert lib().oth_rollout_runner(None, None, 1, 0, 1, None, None, -1, 0, 0, None, None, None, None, None, None,
                                     P(WORK), 4, None) == E
+
+
+def _scratch(fn, *args):
+    tb = ctypes.c_size_t(0)
+    assert fn(*args, None, ctypes.byref(tb), None) == 0
+    temp = np.zeros(max(tb.value, 1), np.uint8)
+    assert fn(*args, P(temp), ctypes.byref(tb), None) == 0
+
+
+def test_td_sort_unpack_and_segments_words_host_build():
+    """Round 5's oth_td_sort_unpack and oth_td_segments_words on the host build
+    of the header, against numpy: the stable key-bit order, the unpacked
+    values, the runs of the sorted keys and the long ones."""
+    rng = np.random.default_rng(3)
+    n = 20000
+    k = rng.integers(0, 300, n).astype(np.uint64) * np.uint64(0x1234567)  # repeats, keys < 2^43
+    vs = rng.integers(-64, 65, n).astype(np.int64)
+    tl = rng.integers(0, 129, n).astype(np.uint64)
+    w = np.ascontiguousarray(((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(43)) | k)
+    lam = np.array([0.9 ** j for j in range(129)], np.float64)
+    keys, vals = np.zeros(n, np.int64), np.zeros(n, np.float64)
+    _scratch(lib().oth_td_sort_unpack, P(w), P(lam), P(keys), P(vals), n)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(keys, k[order].astype(np.int64))
+    np.testing.assert_array_equal(vals, vs[order].astype(np.float64) * lam[tl[order].astype(np.int64)])
+    sw = np.ascontiguousarray(w[order])
+    off, uk, li, cnt, v2 = (np.zeros(n + 1, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int64),
+                            np.zeros(2, np.int64), np.zeros(n, np.float64))
+    _scratch(lib().oth_td_segments_words, P(sw), P(lam), n, 48, P(off), P(uk), P(li), P(cnt), P(v2))
+    np.testing.assert_array_equal(v2, vals)
+    ks = k[order].astype(np.int64)
+    starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
+    assert int(cnt[0]) == len(starts)
+    np.testing.assert_array_equal(off[:len(starts) + 1], np.r_[starts, n])
+    np.testing.assert_array_equal(uk[:len(starts)], ks[starts])
+    want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
+    assert int(cnt[1]) == len(want)
+    np.testing.assert_array_equal(li[:len(want)], want)

@@ -1549,6 +1549,48 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     vals[j + 1] = (double)(-vb) * lam;
 }
 
+// The same updates, one wave per game (round 5): lane p takes the game's
+// positions p, p + 64, ... .  One thread per (g, p) slot of the 129-row stride
+// leaves about half the lanes of the waves that do work idle (a game records
+// ~62 positions of its 129 slots, and the waves straddle games); here a wave
+// idles only on the lanes past the game's own positions.  The game's plies,
+// row offset, base and terminal row are wave-uniform (scalar loads).
+// OTH_TD_UPD_WAVE=0 builds the per-slot kernel for these entry points (A/B).
+#ifndef OTH_TD_UPD_WAVE
+#define OTH_TD_UPD_WAVE 1
+#endif
+__global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __restrict__ pos,
+                                                                 const int64_t* __restrict__ row_off,
+                                                                 const uint8_t* __restrict__ plies,
+                                                                 const int64_t* __restrict__ base,
+                                                                 const double* __restrict__ lam_pow,
+                                                                 int64_t* __restrict__ keys, double* __restrict__ vals,
+                                                                 u64* __restrict__ words, int64_t n) {
+    const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (g >= n) return;
+    const u32 lane = threadIdx.x & 63u;
+    const u32 np = min<u32>(plies[g], OTH_MOVES_STRIDE);
+    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + (row_off ? row_off[g] : g * OTH_POS_STRIDE);
+    const ulonglong2 term = row[np];
+    const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
+    const int64_t jb = base[g];
+    for (u32 p = lane; p <= np; p += 64) {
+        const ulonglong2 b = row[p];
+        const int64_t j = jb + 2 * (int64_t)(np - p);
+        if (words) {
+            const u64 t = (u64)(np - p) << OTH_TD_PACK_TURN_SHIFT;
+            words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_BLACK);
+            words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_WHITE);
+            continue;
+        }
+        const double lam = lam_pow[np - p];
+        keys[j] = td_key(b, OTH_BLACK);
+        vals[j] = (double)vb * lam;
+        keys[j + 1] = td_key(b, OTH_WHITE);
+        vals[j + 1] = (double)(-vb) * lam;
+    }
+}
+
 // one thread per book record, in the learner's own order: row r is update
 // pair 2r ('O') and 2r + 1 ('X'); its book's terminal record (book[0]) is row
 // term_row[r] and l ** turn_left is lam_pow[lam_idx[r]]
@@ -2117,6 +2159,17 @@ DeviceState* device_state() {
 }
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int launched() { return status(hipGetLastError()); }
+// the TD update stream (td_updates_wave_kernel / td_updates_kernel)
+static int td_updates_launch(const u64* pos, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
+                             const double* lam_pow, int64_t* keys, double* vals, u64* words, int64_t n, hipStream_t s) {
+    if (OTH_TD_UPD_WAVE)
+        td_updates_wave_kernel<<<blocks_for(n * 64), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys, vals,
+                                                                     words, n);
+    else
+        td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys,
+                                                                             vals, words, n);
+    return launched();
+}
 
 }  // namespace
 
@@ -2342,29 +2395,22 @@ int oth_td_updates(const uint64_t* pos_boards, const uint8_t* plies, const int64
                    int64_t* keys, double* values, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !lam_pow || !keys || !values))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, nullptr, plies,
-                                                                                          base, lam_pow, keys, values,
-                                                                                          nullptr, n);
-    return launched();
+    return td_updates_launch(pos_boards, nullptr, plies, base, lam_pow, keys, values, nullptr, n, (hipStream_t)stream);
 }
 
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!pos_boards || !plies || !base || !words))) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(
-        pos_boards, row_off, plies, base, nullptr, nullptr, nullptr, reinterpret_cast<u64*>(words), n);
-    return launched();
+    return td_updates_launch(pos_boards, row_off, plies, base, nullptr, nullptr, nullptr, reinterpret_cast<u64*>(words),
+                             n, (hipStream_t)stream);
 }
 int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                         const double* lam_pow, int64_t* keys, double* values, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!pos_boards || !row_off || !plies || !base || !lam_pow || !keys || !values)))
         return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, (hipStream_t)stream>>>(pos_boards, row_off, plies,
-                                                                                          base, lam_pow, keys, values,
-                                                                                          nullptr, n);
-    return launched();
+    return td_updates_launch(pos_boards, row_off, plies, base, lam_pow, keys, values, nullptr, n, (hipStream_t)stream);
 }
 
 int oth_td_updates_records(const uint64_t* rows, const int64_t* term_row, const int32_t* lam_idx,

@@ -1,8 +1,8 @@
 """The TD state-map update of bench.py's td_state_map line, for a kernel trace
 (diagnostic; run on the GPU box under rocprofv3 --kernel-trace --stats):
 three 262,144-game batches of GPU self-play books into one StateMap (the empty
-table, then two merges), each replayed then applied; prints the wall time of
-each update."""
+table, then two merges), each replayed (packed rows, as bench.py) then applied; prints the wall time
+of each replay + update."""
 import os
 import sys
 import time
@@ -26,7 +26,8 @@ for k in range(reps):
     r = ops.rollout(games, 0x5EED, (1 << 41) + k * games, "random", record_moves=True, device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n = sm.update(ops.replay(r.moves, r.plies).boards, r.plies)
+    pk = ops.replay_rows(r.moves, r.plies)
+    n = sm.update(pk.boards, r.plies, pk.row_off)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print("batch %d: %d updates, %d keys, %.2f ms, %.3e updates/s" % (k, n, len(sm), dt * 1e3, n / dt), flush=True)

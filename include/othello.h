@@ -321,26 +321,38 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
 /* Packed updates (the GPU books' path, StateMap.update): the update stream
  * of oth_td_updates / oth_td_updates_rows (row_off NULL: the strided table)
  * with each update as one uint64 word,
- *   (value_side + 64) << 56 | turn_left << 43 | OTH_TD_KEY,
+ *   (value_side + 64) << 56 | turn_left << 36 | OTH_TD_SKEY,
  * turn_left = min(plies[g], OTH_MOVES_STRIDE) - p (0..128; the clamp
  * oth_td_updates applies too), value_side = +-(n_black - n_white) of
  * the terminal: the value is value_side * lam_pow[turn_left], exactly the
  * double oth_td_updates writes, and oth_td_unpack recomputes it.  Half the
  * bytes of a (key, value) pair, and the grouping sort becomes a keys-only
- * sort of these words by their low OTH_TD_KEY_BITS (oth_td_sort_packed):
- * the payload rides along in the word's top bits. */
-#define OTH_TD_PACK_TURN_SHIFT 43
+ * sort of these words by their low OTH_TD_SKEY_BITS (oth_td_sort_packed):
+ * the payload rides along in the word's top bits.
+ * OTH_TD_SKEY (round 5; round 4's words held the OTH_TD_KEY itself in 43
+ * bits): the same counts() tuple numbered in an order-preserving mixed radix
+ * of 36 bits, so the sort takes four radix passes of 9 bits, not five.  With
+ * d discs, m moves (m <= 64 - d) and region counts r_a..r_h,
+ *   OTH_TD_SKEY = (tri(d) + m) * 20138625 + (((((((r_a * 9 + r_b) * 5 + r_c)
+ *                 * 9 + r_d) * 9 + r_e) * 17 + r_f) * 5 + r_g) * 13 + r_h),
+ *   tri(d) = 65 d - d (d - 1) / 2
+ * (the region digits' bases are the region sizes + 1).  Skey order == key
+ * order; the entry points that hand keys back (oth_td_unpack,
+ * oth_td_sort_unpack, oth_td_segments_words) convert to OTH_TD_KEY. */
+#define OTH_TD_SKEY_BITS 36
+#define OTH_TD_PACK_TURN_SHIFT 36
+#define OTH_TD_PACK_TURN_MASK 0xFFFFFu
 #define OTH_TD_PACK_VALUE_SHIFT 56
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream);
-/* Stable sort of n packed words by bits 0..OTH_TD_KEY_BITS-1 (the key):
+/* Stable sort of n packed words by bits 0..OTH_TD_SKEY_BITS-1 (the skey):
  * equal keys keep their stream order; words_out distinct from words_in.
  * temp / temp_bytes as oth_td_sort_pairs.  (The build's own LSD radix sort,
  * round 5; round 4 called rocPRIM's.) */
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream);
 /* oth_td_sort_packed followed by oth_td_unpack in one: the sorted words'
- * keys and values (keys[i] = the i-th sorted word's low OTH_TD_KEY_BITS,
+ * keys and values (keys[i] = the OTH_TD_KEY of the i-th sorted word's skey,
  * values[i] = value_side * lam_pow[turn_left]), the last radix pass writing
  * them directly.  keys distinct from words_in.  temp / temp_bytes as
  * oth_td_sort_pairs (round 5). */
@@ -358,8 +370,8 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
  * nonzero (and their two host syncs). */
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
                     int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream);
-/* oth_td_segments over the key-sorted packed words themselves (each read as
- * its low OTH_TD_KEY_BITS), also writing values[i] = value_side *
+/* oth_td_segments over the skey-sorted packed words themselves (each read as
+ * its low OTH_TD_SKEY_BITS; ukeys receives OTH_TD_KEY values), also writing values[i] = value_side *
  * lam_pow[turn_left] of word i (oth_td_unpack's rule), so a sorted word
  * stream needs no unpack pass: the keys array oth_td_segments reads is never
  * formed (round 5).  values: n doubles (device); the rest as oth_td_segments. */
@@ -373,7 +385,7 @@ int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t 
 int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
                       void* stream);
 
-/* Packed words -> keys[i] = the word's low OTH_TD_KEY_BITS and values[i] =
+/* Packed words -> keys[i] = the OTH_TD_KEY of the word's skey and values[i] =
  * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device). */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                   void* stream);

@@ -216,6 +216,37 @@ static int64_t td_key(const uint8_t f[10]) {
     return k;
 }
 
+/* the packed words' sort key, include/othello.h OTH_TD_SKEY: (discs, moves)
+ * numbered row by row of the triangle moves <= 64 - discs, then the regions as
+ * mixed-radix digits (bases: region sizes + 1), a most significant */
+static const uint64_t skey_base[8] = {5, 9, 5, 9, 9, 17, 5, 13};
+static uint64_t td_skey(const uint8_t f[10]) {
+    uint64_t pair = 0;
+    for (int d = 0; d < f[0]; d++) pair += (uint64_t)(65 - d);
+    pair += f[1];
+    uint64_t reg = 0, scale = 1;
+    for (int i = 7; i >= 0; i--) {
+        reg += (uint64_t)f[2 + i] * scale;
+        scale *= skey_base[i];
+    }
+    return pair * scale + reg;
+}
+static int64_t td_key_of_skey(uint64_t s) {
+    uint64_t scale = 1;
+    for (int i = 0; i < 8; i++) scale *= skey_base[i];
+    uint64_t pair = s / scale, reg = s % scale;
+    uint8_t f[10];
+    int d = 0;
+    while (pair >= (uint64_t)(65 - d)) pair -= (uint64_t)(65 - d++);
+    f[0] = (uint8_t)d;
+    f[1] = (uint8_t)pair;
+    for (int i = 7; i >= 0; i--) {
+        f[2 + i] = (uint8_t)(reg % skey_base[i]);
+        reg /= skey_base[i];
+    }
+    return td_key(f);
+}
+
 static int td_updates_any(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, const double* lam_pow, int64_t* keys, double* values, int64_t n) {
     for (int64_t g = 0; g < n; g++) {
@@ -258,7 +289,7 @@ int oth_td_updates_rows(const uint64_t* pos_boards, const int64_t* row_off, cons
     return td_updates_any(pos_boards, row_off, plies, base, lam_pow, keys, values, n);
 }
 
-/* packed words: the same updates, (value_side + 64) << 56 | turn_left << 43 | OTH_TD_KEY */
+/* packed words: the same updates, (value_side + 64) << 56 | turn_left << 36 | OTH_TD_SKEY */
 int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, const uint8_t* plies,
                           const int64_t* base, uint64_t* words, int64_t n, void* stream) {
     (void)stream;
@@ -276,8 +307,8 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
             const int64_t j = base[g] + 2 * (int64_t)(np - p);
             const uint64_t tl = (uint64_t)(np - p);
             const uint64_t t = tl << OTH_TD_PACK_TURN_SHIFT;
-            words[j] = ((uint64_t)(d + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (uint64_t)td_key(f[0]);
-            words[j + 1] = ((uint64_t)(64 - d) << OTH_TD_PACK_VALUE_SHIFT) | t | (uint64_t)td_key(f[1]);
+            words[j] = ((uint64_t)(d + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey(f[0]);
+            words[j + 1] = ((uint64_t)(64 - d) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey(f[1]);
         }
     }
     return OTH_OK;
@@ -288,9 +319,9 @@ int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, d
     (void)stream;
     if (n < 0 || (n > 0 && (!words || !lam_pow || !keys || !values))) return OTH_EINVAL;
     for (int64_t i = 0; i < n; i++) {
-        keys[i] = (int64_t)(words[i] & ((1ull << OTH_TD_KEY_BITS) - 1));
+        keys[i] = td_key_of_skey(words[i] & ((1ull << OTH_TD_SKEY_BITS) - 1));
         values[i] = (double)((int)(words[i] >> OTH_TD_PACK_VALUE_SHIFT) - 64) *
-                    lam_pow[(words[i] >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
+                    lam_pow[(words[i] >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
     }
     return OTH_OK;
 }
@@ -447,8 +478,8 @@ int oth_td_sort_pairs(const int64_t* keys_in, const double* vals_in, int64_t* ke
 }
 
 /* stable sort of packed words by their key bits: the pairs' merge sort over
- * the words' low OTH_TD_KEY_BITS with the words as the payload */
-#define KEY_MASK ((1ull << OTH_TD_KEY_BITS) - 1)
+ * the words' low OTH_TD_SKEY_BITS with the words as the payload */
+#define KEY_MASK ((1ull << OTH_TD_SKEY_BITS) - 1)
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream) {
     (void)stream;

@@ -21,7 +21,8 @@ N_FEATURES = 10
 POLICY_RANDOM, POLICY_GREEDY, POLICY_EVAL = 0, 1, 2
 EVAL_PHASES, EVAL_FEATURES, EVAL_WEIGHTS = 4, 9, 36
 TD_KEY_BITS = 43
-TD_PACK_TURN_SHIFT = 43   # include/othello.h packed update words
+TD_SKEY_BITS = 36         # include/othello.h packed update words: the sort key's bits
+TD_PACK_TURN_SHIFT = 36
 TD_PACK_VALUE_SHIFT = 56
 TD_FIT_BLOCKS, TD_FIT_COLS = 1024, 64
 

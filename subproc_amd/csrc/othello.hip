@@ -32,6 +32,7 @@
 
 #include "../../include/othello.h"
 #include "bitboard.hpp"
+#include "td_skey.hpp"
 
 #define OTH_VERSION "subproc_amd 0.1.0 gfx950"
 
@@ -1513,6 +1514,15 @@ __device__ __forceinline__ int64_t td_key(ulonglong2 b, u32 sd) {
     for (int r = 0; r < 8; r++) k |= (u64)__popcll(mine & kRegionMasks[r]) << kShift[r];
     return (int64_t)k;
 }
+// the same counts() as the packed words' sort key (td_skey.hpp)
+__device__ __forceinline__ u64 td_skey_of(ulonglong2 b, u32 sd) {
+    u64 mine, mob;
+    side_view(b, sd, mine, mob);
+    u32 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) r[k] = (u32)__popcll(mine & kRegionMasks[k]);
+    return td_skey::encode((u32)__popcll(b.x | b.y), (u32)__popcll(mob), r);
+}
 
 // one thread per recorded position (g, p); rows of an oth_replay table
 // (row_off == nullptr: row g*OTH_POS_STRIDE + p) or of an oth_replay_rows one
@@ -1538,8 +1548,8 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
     if (words) {  // oth_td_updates_packed: (key, value_side, turn_left) in one word
         const u64 tl = np - p;
         const u64 t = tl << OTH_TD_PACK_TURN_SHIFT;
-        words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_BLACK);
-        words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_WHITE);
+        words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
+        words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
         return;
     }
     const double lam = lam_pow[np - p];
@@ -1579,8 +1589,8 @@ __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __re
         const int64_t j = jb + 2 * (int64_t)(np - p);
         if (words) {
             const u64 t = (u64)(np - p) << OTH_TD_PACK_TURN_SHIFT;
-            words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_BLACK);
-            words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | (u64)td_key(b, OTH_WHITE);
+            words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
+            words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
             continue;
         }
         const double lam = lam_pow[np - p];

@@ -10,7 +10,9 @@
 //
 // The sort:
 // rocPRIM's onesweep radix sort of the pairs themselves over the key's 43 bits
-// (OTH_TD_KEY_BITS), in 5 passes of 9-bit digits.  Round 3's key spent 5 bits
+// (OTH_TD_KEY_BITS), in 5 passes of 9-bit digits; the packed words of the GPU
+// books' path over their 36-bit sort key (OTH_TD_SKEY_BITS, td_skey.hpp; round
+// 5), 4 passes.  Round 3's key spent 5 bits
 // on every region count and took 54 bits, 6 passes: 1.93 ms for 32.2M pairs
 // (the gfx950 default of 8 bits a pass took 7 passes, 2.11-2.13 ms,
 // tools/diag/sort_bits.hip; 10 bits ran 3.58 ms, 11 do not fit the LDS).
@@ -24,6 +26,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include "../../include/othello.h"
+#include "td_skey.hpp"
 
 namespace {
 
@@ -54,8 +57,8 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
     if (i >= n) return;
     const uint64_t w = words[i];
     const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
-    keys[i] = (int64_t)(w & ((1ull << OTH_TD_KEY_BITS) - 1));
-    values[i] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
+    keys[i] = td_skey::to_key(w & ((1ull << OTH_TD_SKEY_BITS) - 1));
+    values[i] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
 }
 
 // ---------------------------------------------------------------------------
@@ -515,8 +518,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         const int64_t pos = OTH_SORT_DIAG_LINEAR ? t0 + s : gbase[sort_digit(w, shift, dmask)] + s;
         if (UNPACK) {
             const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
-            keys_out[pos] = (int64_t)(w & ((1ull << OTH_TD_KEY_BITS) - 1));
-            vals_out[pos] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & 0x1fffu];
+            keys_out[pos] = td_skey::to_key(w & ((1ull << OTH_TD_SKEY_BITS) - 1));
+            vals_out[pos] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
         } else {
             out[pos] = w;
         }
@@ -953,9 +956,10 @@ constexpr int kSegWavesPerBlock = kSegBlock / 64;
 // both in order.  (The long keys by atomic appends instead: 25k appends to
 // one counter cost the write pass 83 -> 368 us.)
 // WORDS (oth_td_segments_words, round 5): the input is the key-sorted packed
-// words themselves, each read as its key (the low OTH_TD_KEY_BITS), and the
-// write pass also writes every update's value (oth_td_unpack's rule), so the
-// sorted stream needs no separate unpack into a keys array and a values array.
+// words themselves, each read as its skey (the low OTH_TD_SKEY_BITS; ukeys get
+// the OTH_TD_KEY), and the write pass also writes every update's value
+// (oth_td_unpack's rule), so the sorted stream needs no separate unpack into a
+// keys array and a values array.
 template <bool WRITE, bool WORDS = false>
 __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __restrict__ keys, int64_t n,
                                                            int64_t* __restrict__ wave_cnt,
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
                                                            const double* __restrict__ lam_pow = nullptr,
                                                            double* __restrict__ values = nullptr) {
     __shared__ int64_t stage[kSegWavesPerBlock][kSegWaveKeys + 64];
-    constexpr int64_t kKeyMask = (1ll << OTH_TD_KEY_BITS) - 1;
+    constexpr int64_t kKeyMask = (1ll << OTH_TD_SKEY_BITS) - 1;
     auto key_of = [](int64_t x) { return WORDS ? (x & kKeyMask) : x; };
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
@@ -998,7 +1002,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         const int64_t i = base + r * 64 + lane;
         if (WORDS && WRITE && i < n) {
             const int vs = (int)(payload[r] >> (OTH_TD_PACK_VALUE_SHIFT - OTH_TD_PACK_TURN_SHIFT)) - 64;
-            values[i] = (double)vs * lam_pow[payload[r] & 0x1fffu];
+            values[i] = (double)vs * lam_pow[payload[r] & OTH_TD_PACK_TURN_MASK];
         }
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
@@ -1010,7 +1014,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
             const int64_t at =
                 pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             seg_off[at] = i;
-            ukeys[at] = k[r];
+            ukeys[at] = WORDS ? td_skey::to_key((uint64_t)k[r]) : k[r];
             if (lng)
                 long_idx[lpos + __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u))] = at;
@@ -1156,7 +1160,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     if (!temp) {  // size query: no work, no launch
         size_t bytes = 0;
         const hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, bytes, words_in, words_out, (size_t)n,
-                                                                  0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+                                                                  0, OTH_TD_SKEY_BITS, (hipStream_t)stream);
         *temp_bytes = bytes;
         return e == hipSuccess ? OTH_OK : -(int)e;
     }
@@ -1164,10 +1168,10 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     if (n == 0) return OTH_OK;
     size_t bytes = *temp_bytes;
     const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
-                                                              0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+                                                              0, OTH_TD_SKEY_BITS, (hipStream_t)stream);
     return e == hipSuccess ? OTH_OK : -(int)e;
 #else
-    const size_t need = sort_plan(n, OTH_TD_KEY_BITS).bytes;
+    const size_t need = sort_plan(n, OTH_TD_SKEY_BITS).bytes;
     if (!temp) {  // size query: no work, no launch
         *temp_bytes = need;
         return OTH_OK;
@@ -1176,7 +1180,7 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     if (n >= (1ll << 32)) return OTH_EINVAL;  // 32-bit counts
     if (*temp_bytes < need) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-    const hipError_t e = sort_words(words_in, words_out, n, OTH_TD_KEY_BITS, nullptr, nullptr, nullptr, temp,
+    const hipError_t e = sort_words(words_in, words_out, n, OTH_TD_SKEY_BITS, nullptr, nullptr, nullptr, temp,
                                     (hipStream_t)stream);
     return e == hipSuccess ? OTH_OK : -(int)e;
 #endif
@@ -1189,12 +1193,12 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
     // rocPRIM's sort of the words into the scratch, then the unpack kernel
     size_t sort_bytes = 0;
     hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, sort_bytes, words_in, (uint64_t*)nullptr, (size_t)n,
-                                                        0, OTH_TD_KEY_BITS, (hipStream_t)stream);
+                                                        0, OTH_TD_SKEY_BITS, (hipStream_t)stream);
     if (e != hipSuccess) return -(int)e;
     sort_bytes = (sort_bytes + 255) / 256 * 256;
     const size_t need = sort_bytes + (size_t)std::max<int64_t>(n, 1) * sizeof(uint64_t);
 #else
-    const size_t need = sort_plan(n, OTH_TD_KEY_BITS).bytes;
+    const size_t need = sort_plan(n, OTH_TD_SKEY_BITS).bytes;
 #endif
     if (!temp) {  // size query: no work, no launch
         *temp_bytes = need;
@@ -1208,13 +1212,13 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
     if (n == 0) return OTH_OK;
 #if OTH_SORT_ROCPRIM
     uint64_t* sorted = reinterpret_cast<uint64_t*>(static_cast<char*>(temp) + sort_bytes);
-    e = rocprim::radix_sort_keys<SortConfig>(temp, sort_bytes, words_in, sorted, (size_t)n, 0, OTH_TD_KEY_BITS,
+    e = rocprim::radix_sort_keys<SortConfig>(temp, sort_bytes, words_in, sorted, (size_t)n, 0, OTH_TD_SKEY_BITS,
                                              (hipStream_t)stream);
     if (e != hipSuccess) return -(int)e;
     td_unpack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(sorted, lam_pow, keys, values, n);
     e = hipGetLastError();
 #else
-    const hipError_t e = sort_words(words_in, nullptr, n, OTH_TD_KEY_BITS, lam_pow, keys, values, temp,
+    const hipError_t e = sort_words(words_in, nullptr, n, OTH_TD_SKEY_BITS, lam_pow, keys, values, temp,
                                     (hipStream_t)stream);
 #endif
     return e == hipSuccess ? OTH_OK : -(int)e;

@@ -76,6 +76,54 @@ def key_to_counts(k):
     return tuple((k >> s) & ((1 << w) - 1) for s, w in zip(_SHIFTS, _WIDTH))
 
 
+# include/othello.h OTH_TD_SKEY (the packed words' 36-bit sort key): (discs,
+# moves) numbered along the triangle moves <= 64 - discs, the region counts as
+# mixed-radix digits of bases region size + 1
+_SKEY_BASES = (5, 9, 5, 9, 9, 17, 5, 13)
+_SKEY_REGIONS = 20138625
+
+
+def counts_to_skey(c):
+    """A counts() 10-tuple's OTH_TD_SKEY (same order as counts_to_key)."""
+    d, m = int(c[0]), int(c[1])
+    if not (0 <= d <= 64 and 0 <= m <= 64 - d):
+        raise ValueError(f"counts ({d}, {m}) outside moves <= 64 - discs")
+    reg = 0
+    for v, b in zip(c[2:], _SKEY_BASES):
+        if not 0 <= int(v) < b:
+            raise ValueError(f"region count {v} out of range")
+        reg = reg * b + int(v)
+    return (65 * d - d * (d - 1) // 2 + m) * _SKEY_REGIONS + reg
+
+
+SKEY_LIMIT = 2145 * _SKEY_REGIONS  # every integer below it is a valid OTH_TD_SKEY
+_TRI = np.array([65 * d - d * (d - 1) // 2 for d in range(66)], np.int64)
+
+
+def skeys_to_keys(s):
+    """OTH_TD_SKEY values -> OTH_TD_KEY values (numpy, vectorised)."""
+    pair, reg = np.divmod(np.asarray(s, dtype=np.int64), _SKEY_REGIONS)
+    d = np.searchsorted(_TRI, pair, side="right") - 1
+    key = (d << _SHIFTS[0]) | ((pair - _TRI[d]) << _SHIFTS[1])
+    for b, sh in zip(reversed(_SKEY_BASES), reversed(_SHIFTS[2:])):
+        reg, v = np.divmod(reg, b)
+        key |= v << sh
+    return key
+
+
+def skey_to_counts(s):
+    pair, reg = divmod(int(s), _SKEY_REGIONS)
+    d = 0
+    while pair >= 65 - d:
+        pair -= 65 - d
+        d += 1
+    regs = []
+    for b in reversed(_SKEY_BASES):
+        reg, v = divmod(reg, b)
+        regs.append(v)
+    return (d, pair, *reversed(regs))
+
+
 def unpack_counts(keys):
     """Packed keys (device int64 tensor) -> (n, 10) int64 counts() tuples."""
     cols = [(keys >> s) & ((1 << w) - 1) for s, w in zip(_SHIFTS, _WIDTH)]
@@ -257,13 +305,18 @@ class StateMap:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
             n_upd = ukeys.numel()
-            is_new = None
+            pending = None
             if len(self):
                 init = torch.empty(n_upd, dtype=torch.float64, device=self.device)
                 is_new = torch.empty(n_upd, dtype=torch.uint8, device=self.device)
                 _with_scratch(lib.oth_td_lookup, (self.keys.data_ptr(), self.values.data_ptr(), len(self),
                                                   ukeys.data_ptr(), n_upd, init.data_ptr(), is_new.data_ptr()),
                               stream, self.device, "oth_td_lookup")
+                # the merge's sizes before the EMA: the host reads the new-key
+                # count while the EMA runs (round 5; a stream sync after the
+                # EMA left the GPU idle while the host sized and launched the
+                # merge)
+                pending = self._new_before(is_new, lib, stream)
             else:
                 init = torch.zeros(n_upd, dtype=torch.float64, device=self.device)
             out = torch.empty_like(init)
@@ -274,21 +327,33 @@ class StateMap:
                                                  1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN,
                                                  long_idx.data_ptr(), long_idx.numel(), sv.numel()),
                           stream, self.device, "oth_td_ema_split")
-            if is_new is None:  # (a copy: ukeys is a view of an n-entry buffer)
+            if pending is None:  # (a copy: ukeys is a view of an n-entry buffer)
                 self.keys, self.values = ukeys.clone(), out
             else:
-                self._merge(is_new, ukeys, out, lib, stream)
+                self._merge(pending, ukeys, out, lib, stream)
 
-    def _merge(self, is_new, ukeys, out, lib, stream):
-        """The batch's keys (sorted, unique; is_new: absent from the table) into
-        the key-sorted table: oth_td_merge (HIP merge path) writes the sorted
-        union, placing every element by rank; new_before[j] = batch keys
-        before j that are new."""
-        n_old, n_upd = len(self), ukeys.numel()
+    def _new_before(self, is_new, lib, stream):
+        """new_before[j] = batch keys before j that are new (oth_td_new_before),
+        and its total copied to pinned host memory behind an event."""
+        n_upd = is_new.numel()
         new_before = torch.empty(n_upd + 1, dtype=torch.int64, device=self.device)
         _with_scratch(lib.oth_td_new_before, (is_new.data_ptr(), n_upd, new_before.data_ptr()), stream, self.device,
                       "oth_td_new_before")
-        n_new = int(new_before[-1])
+        host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        host.copy_(new_before[-1:], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return new_before, host, ev
+
+    def _merge(self, pending, ukeys, out, lib, stream):
+        """The batch's keys (sorted, unique) into the key-sorted table:
+        oth_td_merge (HIP merge path) writes the sorted union, placing every
+        element by rank; new_before[j] = batch keys before j that are absent
+        from the table (pending: _new_before's result)."""
+        new_before, host, ev = pending
+        n_old, n_upd = len(self), ukeys.numel()
+        ev.synchronize()
+        n_new = int(host[0])
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
         _with_scratch(lib.oth_td_merge, (self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(),

@@ -14,6 +14,7 @@ import pytest
 import oracle
 from golden_io import ROLLOUT_FIXTURES, h, load_json, load_npz
 from subproc_amd import _lib
+from subproc_amd.td import skeys_to_keys
 
 P = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
 
@@ -184,26 +185,27 @@ def _scratch(fn, *args):
 
 def test_td_sort_unpack_and_segments_words_host_build():
     """Round 5's oth_td_sort_unpack and oth_td_segments_words on the host build
-    of the header, against numpy: the stable key-bit order, the unpacked
-    values, the runs of the sorted keys and the long ones."""
+    of the header, against numpy: the stable skey-bit order, the keys as
+    OTH_TD_KEY values, the unpacked values, the runs of the sorted keys and the
+    long ones."""
     rng = np.random.default_rng(3)
     n = 20000
-    k = rng.integers(0, 300, n).astype(np.uint64) * np.uint64(0x1234567)  # repeats, keys < 2^43
+    k = rng.integers(0, 300, n).astype(np.uint64) * np.uint64(0x1234567)  # repeats, skeys below SKEY_LIMIT
     vs = rng.integers(-64, 65, n).astype(np.int64)
     tl = rng.integers(0, 129, n).astype(np.uint64)
-    w = np.ascontiguousarray(((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(43)) | k)
+    w = np.ascontiguousarray(((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)) | k)
     lam = np.array([0.9 ** j for j in range(129)], np.float64)
     keys, vals = np.zeros(n, np.int64), np.zeros(n, np.float64)
     _scratch(lib().oth_td_sort_unpack, P(w), P(lam), P(keys), P(vals), n)
     order = np.argsort(k, kind="stable")
-    np.testing.assert_array_equal(keys, k[order].astype(np.int64))
+    np.testing.assert_array_equal(keys, skeys_to_keys(k[order].astype(np.int64)))
     np.testing.assert_array_equal(vals, vs[order].astype(np.float64) * lam[tl[order].astype(np.int64)])
     sw = np.ascontiguousarray(w[order])
     off, uk, li, cnt, v2 = (np.zeros(n + 1, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int64),
                             np.zeros(2, np.int64), np.zeros(n, np.float64))
     _scratch(lib().oth_td_segments_words, P(sw), P(lam), n, 48, P(off), P(uk), P(li), P(cnt), P(v2))
     np.testing.assert_array_equal(v2, vals)
-    ks = k[order].astype(np.int64)
+    ks = skeys_to_keys(k[order].astype(np.int64))
     starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
     assert int(cnt[0]) == len(starts)
     np.testing.assert_array_equal(off[:len(starts) + 1], np.r_[starts, n])

@@ -11,6 +11,7 @@ import torch
 
 import oracle
 from subproc_amd import _lib
+from subproc_amd.td import _SKEY_REGIONS, SKEY_LIMIT, skeys_to_keys
 
 pytestmark = pytest.mark.gpu
 
@@ -95,16 +96,26 @@ def sort_pair(keys, vals, keys_out, vals_out, n):
     same(keys_out, vals_out)
 
 
+def _skeys(rng, size):
+    """Random valid OTH_TD_SKEY values (td.py): any integer below SKEY_LIMIT
+    whose (discs, moves) pair is not (0, 64), which OTH_TD_KEY cannot hold;
+    the first and last valid ones included."""
+    s = rng.integers(0, SKEY_LIMIT - _SKEY_REGIONS, size=size, dtype=np.int64)
+    s[s >= 64 * _SKEY_REGIONS] += _SKEY_REGIONS  # skip pair 64 = (0, 64)
+    if size > 1:
+        s[0], s[-1] = 0, SKEY_LIMIT - 1
+    return s
+
+
 @pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 7), (300001, 5000), (2_000_003, 1 << 20)])
 def test_td_sort_packed_stable(n, distinct):
-    """Packed words with keys over all OTH_TD_KEY_BITS bits and many repeats,
-    the payload bits (the top 21) a stream position: both builds sort by the
-    key bits alone, stably, the payload riding along."""
+    """Packed words with sort keys over the whole OTH_TD_SKEY range and many
+    repeats, the payload bits (the top 28) a stream position: both builds sort
+    by the skey bits alone, stably, the payload riding along."""
     rng = np.random.default_rng(n + 1)
-    pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
-    pool[0], pool[-1] = 0, (1 << _lib.TD_KEY_BITS) - 1
+    pool = _skeys(rng, distinct)
     k = pool[rng.integers(0, distinct, size=n)].astype(np.uint64)
-    w = (np.arange(n, dtype=np.uint64) << np.uint64(_lib.TD_KEY_BITS)) | k  # the payload: stream positions
+    w = (np.arange(n, dtype=np.uint64) << np.uint64(_lib.TD_SKEY_BITS)) | k  # the payload: stream positions
     words, out = Buf(w), Buf(np.zeros(n, np.uint64))
     both_scratch("oth_td_sort_packed", words, out, n)
     same(out)
@@ -116,16 +127,16 @@ def test_td_sort_packed_stable(n, distinct):
 def test_td_sort_unpack_pair(n, distinct, offset):
     """oth_td_sort_unpack (round 5: the sort with the unpack in its last pass)
     on both builds: the keys and values equal the stable sort of the words by
-    key bits followed by oth_td_unpack.  Payloads as oth_td_updates_packed
-    writes them (value_side + 64 in the top byte, turn_left 0..128 below);
-    offset 1: the words start 8 bytes into a device buffer (not 16-B aligned)."""
+    skey bits followed by oth_td_unpack (keys: the skeys as OTH_TD_KEY values).
+    Payloads as oth_td_updates_packed writes them (value_side + 64 in the top
+    byte, turn_left 0..128 below); offset 1: the words start 8 bytes into a
+    device buffer (not 16-B aligned)."""
     rng = np.random.default_rng(n + 7)
-    pool = rng.integers(0, 1 << _lib.TD_KEY_BITS, size=distinct, dtype=np.int64)
-    pool[0], pool[-1] = 0, (1 << _lib.TD_KEY_BITS) - 1
+    pool = _skeys(rng, distinct)
     k = pool[rng.integers(0, distinct, size=n)].astype(np.uint64)
     vs = rng.integers(-64, 65, size=n).astype(np.int64)
     tl = rng.integers(0, 129, size=n).astype(np.uint64)
-    w = (((vs + 64).astype(np.uint64)) << np.uint64(56)) | (tl << np.uint64(43)) | k
+    w = (((vs + 64).astype(np.uint64)) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)) | k
     lam = np.array([0.9 ** j for j in range(129)], np.float64)
     words = Buf(np.concatenate([np.zeros(offset, np.uint64), w]))
     ko, vo, lamb = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64)), Buf(lam)
@@ -142,7 +153,7 @@ def test_td_sort_unpack_pair(n, distinct, offset):
     torch.cuda.synchronize()
     same(ko, vo)
     order = np.argsort(k, kind="stable")
-    np.testing.assert_array_equal(ko.h, k[order].astype(np.int64))
+    np.testing.assert_array_equal(ko.h, skeys_to_keys(k[order].astype(np.int64)))
     np.testing.assert_array_equal(vo.h, vs[order].astype(np.float64) * lam[tl[order].astype(np.int64)])
 
 
@@ -398,7 +409,8 @@ def test_td_pair():
         words = Buf(np.zeros(total, np.uint64))
         both("oth_td_updates_packed", layout, po, plies, base, words, n)
         same(words)
-        np.testing.assert_array_equal((words.h & np.uint64((1 << _lib.TD_KEY_BITS) - 1)).astype(np.int64), keys.h)
+        np.testing.assert_array_equal(skeys_to_keys((words.h & np.uint64((1 << _lib.TD_SKEY_BITS) - 1)).astype(np.int64)),
+                                      keys.h)
         sw = Buf(np.zeros(total, np.uint64))
         both_scratch("oth_td_sort_packed", words, sw, total)
         same(sw)
@@ -450,18 +462,19 @@ def test_td_segments_pair():
 
 
 def test_td_segments_words_pair():
-    """oth_td_segments_words (round 5): the same runs read from key-sorted
-    packed words (payloads in the top 21 bits, which must not split a run),
-    and every word's value as oth_td_unpack gives it, on both builds."""
+    """oth_td_segments_words (round 5): the same runs read from skey-sorted
+    packed words (payloads in the top 28 bits, which must not split a run),
+    the keys handed back as OTH_TD_KEY values, and every word's value as
+    oth_td_unpack gives it, on both builds."""
     rng = np.random.default_rng(13)
     lam = np.array([0.9 ** j for j in range(129)], np.float64)
     for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 1023, 1024, 1025, 5000],
                                                                           400)):
-        keys = np.repeat(np.cumsum(rng.integers(1, 1000, len(lens))).astype(np.uint64), lens)
+        keys = np.repeat(np.cumsum(rng.integers(1, 1 << 20, len(lens))).astype(np.uint64), lens)  # sorted skeys
         n = len(keys)
         vs = rng.integers(-64, 65, n).astype(np.int64)
         tl = rng.integers(0, 129, n).astype(np.uint64)
-        w = ((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(43)) | keys
+        w = ((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)) | keys
         words, lamb = Buf(w), Buf(lam)
         off, uk, li, cnt, val = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)),
                                  Buf(np.zeros(n, np.int64)), Buf(np.zeros(2, np.int64)), Buf(np.zeros(n, np.float64)))
@@ -472,7 +485,8 @@ def test_td_segments_words_pair():
         assert m == len(starts)
         np.testing.assert_array_equal(off.h[:m + 1], np.r_[starts, n])
         np.testing.assert_array_equal(off.d.cpu().numpy()[:m + 1], off.h[:m + 1])
-        np.testing.assert_array_equal(uk.d.cpu().numpy()[:m], keys[starts].astype(np.int64))
+        np.testing.assert_array_equal(uk.d.cpu().numpy()[:m], skeys_to_keys(keys[starts].astype(np.int64)))
+        np.testing.assert_array_equal(uk.h[:m], uk.d.cpu().numpy()[:m])
         np.testing.assert_array_equal(val.h, vs.astype(np.float64) * lam[tl.astype(np.int64)])
         want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
         assert nl == len(want)

@@ -165,3 +165,23 @@ def test_cpu_abi_td_lookup():
     tb, tmp = ctypes.c_size_t(0), np.zeros(1, np.uint8)
     assert lib.oth_td_lookup(P(old), P(ov), 4, P(upd), 5, P(init), P(is_new), P(tmp), ctypes.byref(tb), None) == 0
     assert init.tolist() == [0.0, -1.0, 0.0, 3.5, 0.0] and is_new.tolist() == [1, 0, 1, 0, 1]
+
+
+def test_skey_order_and_round_trip():
+    """include/othello.h OTH_TD_SKEY (the packed words' 36-bit sort key): a
+    bijection on counts() tuples with moves <= 64 - discs that orders them as
+    OTH_TD_KEY does, decoded alike by the scalar and the vectorised helper;
+    every value below SKEY_LIMIT fits 36 bits."""
+    rng = np.random.default_rng(5)
+    cs = [(0,) * 10, (64, 0, 4, 8, 4, 8, 8, 16, 4, 12), (0, 63, 4, 8, 4, 8, 8, 16, 4, 12), (1, 63) + (0,) * 8]
+    for _ in range(5000):
+        d = int(rng.integers(0, 65))
+        cs.append((d, int(rng.integers(0, min(64, 65 - d)))) + tuple(int(rng.integers(0, b)) for b in (5, 9, 5, 9, 9, 17, 5, 13)))
+    keys = np.array([td.counts_to_key(c) for c in cs])
+    skeys = np.array([td.counts_to_skey(c) for c in cs])
+    assert all(td.skey_to_counts(s) == tuple(c) for s, c in zip(skeys, cs))
+    np.testing.assert_array_equal(np.argsort(keys, kind="stable"), np.argsort(skeys, kind="stable"))
+    np.testing.assert_array_equal(td.skeys_to_keys(skeys), keys)
+    assert td.SKEY_LIMIT <= 1 << _lib.TD_SKEY_BITS and skeys.max() == td.SKEY_LIMIT - 1
+    with pytest.raises(ValueError):
+        td.counts_to_skey((10, 55) + (0,) * 8)

@@ -40,7 +40,7 @@ words = torch.empty(n, dtype=torch.int64, device=dev)
 assert libs[1].oth_td_updates_packed(pk.boards.data_ptr(), pk.row_off.data_ptr(), r.plies.data_ptr(), base.data_ptr(),
                                      words.data_ptr(), games, s) == 0
 lam = torch.tensor(lam_pow_table(0.9), dtype=torch.float64, device=dev)
-KEY = (1 << 43) - 1
+KEY = (1 << 36) - 1  # include/othello.h OTH_TD_SKEY_BITS (round 5; 43 before)
 _, perm = torch.sort(words & KEY, stable=True)
 want = words[perm]
 print("words %d" % n, flush=True)

@@ -19,7 +19,7 @@ td = "--td" in sys.argv  # the TD update words of 262,144 random games (skewed k
 sizes = [int(x) for x in sys.argv[2:] if not x.startswith("--")] or [1000, 100_000, 1_000_000, 8_000_000, 32_000_000]
 s = torch.cuda.current_stream().cuda_stream
 g = torch.Generator(device="cuda").manual_seed(1)
-KEY = (1 << 43) - 1
+KEY = (1 << 36) - 1  # include/othello.h OTH_TD_SKEY_BITS (round 5; 43 before)
 if td:
     from subproc_amd import ops
     r = ops.rollout(1 << 18, 0x5EED, 1 << 41, "random", record_moves=True, device="cuda")
@@ -35,7 +35,7 @@ for n in sizes:
         w = W[:n].contiguous()
     else:
         k = torch.randint(0, 1 << 20, (n,), device="cuda", generator=g) * 8388593 & KEY
-        w = k | (torch.arange(n, device="cuda") << 43)
+        w = k | (torch.arange(n, device="cuda") << 36)
     o = torch.empty_like(w)
     tb = ctypes.c_size_t(0)
     assert L.oth_td_sort_packed(w.data_ptr(), o.data_ptr(), n, None, ctypes.byref(tb), s) == 0

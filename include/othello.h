@@ -333,8 +333,8 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
  * bits): the same counts() tuple numbered in an order-preserving mixed radix
  * of 36 bits, so the sort takes four radix passes of 9 bits, not five.  With
  * d discs, m moves (m <= 64 - d) and region counts r_a..r_h,
- *   OTH_TD_SKEY = (tri(d) + m) * 20138625 + (((((((r_a * 9 + r_b) * 5 + r_c)
- *                 * 9 + r_d) * 9 + r_e) * 17 + r_f) * 5 + r_g) * 13 + r_h),
+ *   OTH_TD_SKEY = ((tri(d) + m) * 5 + r_a) << 22
+ *               | ((((((r_b * 5 + r_c) * 9 + r_d) * 9 + r_e) * 17 + r_f) * 5 + r_g) * 13 + r_h),
  *   tri(d) = 65 d - d (d - 1) / 2
  * (the region digits' bases are the region sizes + 1).  Skey order == key
  * order; the entry points that hand keys back (oth_td_unpack,
@@ -371,9 +371,9 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
 int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_off, int64_t* ukeys,
                     int64_t* long_idx, int64_t* counts, void* temp, size_t* temp_bytes, void* stream);
 /* oth_td_segments over the skey-sorted packed words themselves (each read as
- * its low OTH_TD_SKEY_BITS; ukeys receives OTH_TD_KEY values), also writing values[i] = value_side *
- * lam_pow[turn_left] of word i (oth_td_unpack's rule), so a sorted word
- * stream needs no unpack pass: the keys array oth_td_segments reads is never
+ * its low OTH_TD_SKEY_BITS; ukeys receives OTH_TD_KEY values), also
+ * writing values[i] = value_side * lam_pow[turn_left] of word i
+ * (oth_td_unpack's rule), so a sorted word stream needs no unpack pass: the keys array oth_td_segments reads is never
  * formed (round 5).  values: n doubles (device); the rest as oth_td_segments. */
 int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t n, int64_t long_min, int64_t* seg_off,
                           int64_t* ukeys, int64_t* long_idx, int64_t* counts, double* values, void* temp,

@@ -218,31 +218,32 @@ static int64_t td_key(const uint8_t f[10]) {
 
 /* the packed words' sort key, include/othello.h OTH_TD_SKEY: (discs, moves)
  * numbered row by row of the triangle moves <= 64 - discs, then the regions as
- * mixed-radix digits (bases: region sizes + 1), a most significant */
+ * mixed-radix digits (bases: region sizes + 1), a most significant; the
+ * number split as (pair, a) << 22 | (b..h) */
 static const uint64_t skey_base[8] = {5, 9, 5, 9, 9, 17, 5, 13};
 static uint64_t td_skey(const uint8_t f[10]) {
     uint64_t pair = 0;
     for (int d = 0; d < f[0]; d++) pair += (uint64_t)(65 - d);
     pair += f[1];
-    uint64_t reg = 0, scale = 1;
-    for (int i = 7; i >= 0; i--) {
-        reg += (uint64_t)f[2 + i] * scale;
+    uint64_t low = 0, scale = 1;
+    for (int i = 7; i >= 1; i--) {
+        low += (uint64_t)f[2 + i] * scale;
         scale *= skey_base[i];
     }
-    return pair * scale + reg;
+    return ((pair * skey_base[0] + f[2]) << 22) | low;
 }
 static int64_t td_key_of_skey(uint64_t s) {
-    uint64_t scale = 1;
-    for (int i = 0; i < 8; i++) scale *= skey_base[i];
-    uint64_t pair = s / scale, reg = s % scale;
+    uint64_t high = s >> 22, low = s & ((1ull << 22) - 1);
     uint8_t f[10];
+    uint64_t pair = high / skey_base[0];
+    f[2] = (uint8_t)(high % skey_base[0]);
     int d = 0;
     while (pair >= (uint64_t)(65 - d)) pair -= (uint64_t)(65 - d++);
     f[0] = (uint8_t)d;
     f[1] = (uint8_t)pair;
-    for (int i = 7; i >= 0; i--) {
-        f[2 + i] = (uint8_t)(reg % skey_base[i]);
-        reg /= skey_base[i];
+    for (int i = 7; i >= 1; i--) {
+        f[2 + i] = (uint8_t)(low % skey_base[i]);
+        low /= skey_base[i];
     }
     return td_key(f);
 }

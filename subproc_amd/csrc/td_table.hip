@@ -621,6 +621,40 @@ constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
 constexpr int kLookupK = 8;
 constexpr int kLookupTile = kMergeBlock * kLookupK;
 
+// A merge tile's inputs into LDS: A[a0, a0 + na) then B[b0, b0 + n - na)
+// (keys, and values when Av / sv are given), every load of the thread in
+// flight before its first LDS store (round 5: the strided loops these replace
+// waited for each load before issuing the next -- the merge and lookup ran at
+// ~3 TB/s, latency-bound)
+template <int K>
+__device__ __forceinline__ void stage_tile(const int64_t* __restrict__ A, const double* __restrict__ Av, int64_t a0,
+                                           int na, const int64_t* __restrict__ B, const double* __restrict__ Bv,
+                                           int64_t b0, int n, int64_t* sk, double* sv) {
+    int64_t kk[K];
+    double vv[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const int e = (int)threadIdx.x + q * kMergeBlock;
+        kk[q] = 0;
+        vv[q] = 0.0;
+        if (e < na) {
+            kk[q] = A[a0 + e];
+            if (Av) vv[q] = Av[a0 + e];
+        } else if (e < n) {
+            kk[q] = B[b0 + (e - na)];
+            if (Bv) vv[q] = Bv[b0 + (e - na)];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const int e = (int)threadIdx.x + q * kMergeBlock;
+        if (e < n) {
+            sk[e] = kk[q];
+            if (sv) sv[e] = vv[q];
+        }
+    }
+}
+
 // The merge-path splits of every tile, one thread each, in a kernel of their
 // own (the partition step of a merge path): split[s] is the first i in
 // [max(0, d - nB), min(d, nA)] with A[i] >= B[d - i - 1] for diagonal
@@ -678,16 +712,9 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     const int64_t s0 = split[blockIdx.x], s1 = split[blockIdx.x + 1];  // the tile's ends in A
     const int64_t a0 = s0, b0 = d0 - a0;
     const int na = (int)(s1 - a0), nb = (int)(d1 - s1 - b0);
-    for (int k = tid; k < na; k += kMergeBlock) {
-        sk[k] = A[a0 + k];
-        sv[k] = Av[a0 + k];
-    }
-    for (int k = tid; k < nb; k += kMergeBlock) {
-        sk[na + k] = B[b0 + k];
-        sv[na + k] = Bv[b0 + k];
-    }
-    __syncthreads();
     const int n = na + nb;
+    stage_tile<kMergeK>(A, Av, a0, na, B, Bv, b0, n, sk, sv);
+    __syncthreads();
     const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
     int lo = t0 > nb ? t0 - nb : 0, hi = t0 < na ? t0 : na;
     while (lo < hi) {
@@ -789,9 +816,13 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     }
     __syncthreads();
     const int cnt_out = (int)(end - base);  // <= kMergeTile: one slot per merged position at most
-    for (int k = tid; k < cnt_out; k += kMergeBlock) {
-        out_k[base + k] = sk[k];
-        out_v[base + k] = sv[k];
+#pragma unroll
+    for (int q = 0; q < kMergeK; q++) {
+        const int k = tid + q * kMergeBlock;
+        if (k < cnt_out) {
+            out_k[base + k] = sk[k];
+            out_v[base + k] = sv[k];
+        }
     }
 }
 
@@ -816,10 +847,9 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
     const int64_t s0 = split[blockIdx.x], s1 = split[blockIdx.x + 1];
     const int64_t a0 = s0, b0 = d0 - a0;
     const int na = (int)(s1 - a0), nb = (int)(d1 - s1 - b0);
-    for (int k = tid; k < na; k += kMergeBlock) sk[k] = A[a0 + k];
-    for (int k = tid; k < nb; k += kMergeBlock) sk[na + k] = B[b0 + k];
-    __syncthreads();
     const int n = na + nb;
+    stage_tile<kLookupK>(A, nullptr, a0, na, B, nullptr, b0, n, sk, nullptr);
+    __syncthreads();
     const int t0 = min(tid * kLookupK, n), t1 = min(t0 + kLookupK, n);
     int lo = t0 > nb ? t0 - nb : 0, hi = t0 < na ? t0 : na;
     while (lo < hi) {
@@ -842,10 +872,21 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
     __syncthreads();
     // the hits' values loaded here, all in flight at once, not one per step of
     // the merge loop above (round 4)
-    for (int k = tid; k < nb; k += kMergeBlock) {
-        const int r = shit[k];
-        init[b0 + k] = r >= 0 ? Av[a0 + r] : 0.0;
-        is_new[b0 + k] = r >= 0 ? 0 : 1;
+    // (unrolled: every hit's load in flight before the first store; round 5)
+    double hv[kLookupK];
+#pragma unroll
+    for (int q = 0; q < kLookupK; q++) {
+        const int k = tid + q * kMergeBlock;
+        const int r = k < nb ? shit[k] : -1;
+        hv[q] = r >= 0 ? Av[a0 + r] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kLookupK; q++) {
+        const int k = tid + q * kMergeBlock;
+        if (k < nb) {
+            init[b0 + k] = hv[q];
+            is_new[b0 + k] = shit[k] >= 0 ? 0 : 1;
+        }
     }
 }
 

@@ -78,9 +78,11 @@ def key_to_counts(k):
 
 # include/othello.h OTH_TD_SKEY (the packed words' 36-bit sort key): (discs,
 # moves) numbered along the triangle moves <= 64 - discs, the region counts as
-# mixed-radix digits of bases region size + 1
+# mixed-radix digits of bases region size + 1; (pair, region a) << 22 | (b..h)
 _SKEY_BASES = (5, 9, 5, 9, 9, 17, 5, 13)
-_SKEY_REGIONS = 20138625
+_SKEY_LOW = 22
+SKEY_LIMIT = (2145 * 5) << _SKEY_LOW  # the skeys lie below it (not every value below is one)
+_TRI = np.array([65 * d - d * (d - 1) // 2 for d in range(66)], np.int64)
 
 
 def counts_to_skey(c):
@@ -88,40 +90,30 @@ def counts_to_skey(c):
     d, m = int(c[0]), int(c[1])
     if not (0 <= d <= 64 and 0 <= m <= 64 - d):
         raise ValueError(f"counts ({d}, {m}) outside moves <= 64 - discs")
-    reg = 0
     for v, b in zip(c[2:], _SKEY_BASES):
         if not 0 <= int(v) < b:
             raise ValueError(f"region count {v} out of range")
-        reg = reg * b + int(v)
-    return (65 * d - d * (d - 1) // 2 + m) * _SKEY_REGIONS + reg
-
-
-SKEY_LIMIT = 2145 * _SKEY_REGIONS  # every integer below it is a valid OTH_TD_SKEY
-_TRI = np.array([65 * d - d * (d - 1) // 2 for d in range(66)], np.int64)
+    low = 0
+    for v, b in zip(c[3:], _SKEY_BASES[1:]):
+        low = low * b + int(v)
+    return (((65 * d - d * (d - 1) // 2 + m) * 5 + int(c[2])) << _SKEY_LOW) | low
 
 
 def skeys_to_keys(s):
     """OTH_TD_SKEY values -> OTH_TD_KEY values (numpy, vectorised)."""
-    pair, reg = np.divmod(np.asarray(s, dtype=np.int64), _SKEY_REGIONS)
+    s = np.asarray(s, dtype=np.int64)
+    pair, ra = np.divmod(s >> _SKEY_LOW, 5)
+    low = s & ((1 << _SKEY_LOW) - 1)
     d = np.searchsorted(_TRI, pair, side="right") - 1
-    key = (d << _SHIFTS[0]) | ((pair - _TRI[d]) << _SHIFTS[1])
-    for b, sh in zip(reversed(_SKEY_BASES), reversed(_SHIFTS[2:])):
-        reg, v = np.divmod(reg, b)
+    key = (d << _SHIFTS[0]) | ((pair - _TRI[d]) << _SHIFTS[1]) | (ra << _SHIFTS[2])
+    for b, sh in zip(reversed(_SKEY_BASES[1:]), reversed(_SHIFTS[3:])):
+        low, v = np.divmod(low, b)
         key |= v << sh
     return key
 
 
 def skey_to_counts(s):
-    pair, reg = divmod(int(s), _SKEY_REGIONS)
-    d = 0
-    while pair >= 65 - d:
-        pair -= 65 - d
-        d += 1
-    regs = []
-    for b in reversed(_SKEY_BASES):
-        reg, v = divmod(reg, b)
-        regs.append(v)
-    return (d, pair, *reversed(regs))
+    return key_to_counts(int(skeys_to_keys(np.array([int(s)]))[0]))
 
 
 def unpack_counts(keys):

@@ -183,6 +183,18 @@ def _scratch(fn, *args):
     assert fn(*args, P(temp), ctypes.byref(tb), None) == 0
 
 
+def _skeys(rng, size):
+    """Random OTH_TD_SKEY values (include/othello.h): (pair, region a) << 22 |
+    the regions b..h in their mixed radix, pair (discs, moves) 64 = (0, 64)
+    left out (OTH_TD_KEY cannot hold it); the first and last skeys included."""
+    hi = rng.integers(0, 2144 * 5, size=size, dtype=np.int64)
+    hi[hi >= 64 * 5] += 5
+    s = (hi << 22) | rng.integers(0, 4027725, size=size, dtype=np.int64)
+    if size > 1:
+        s[0], s[-1] = 0, ((2145 * 5 - 1) << 22) | (4027725 - 1)
+    return s
+
+
 def test_td_sort_unpack_and_segments_words_host_build():
     """Round 5's oth_td_sort_unpack and oth_td_segments_words on the host build
     of the header, against numpy: the stable skey-bit order, the keys as
@@ -190,7 +202,7 @@ def test_td_sort_unpack_and_segments_words_host_build():
     long ones."""
     rng = np.random.default_rng(3)
     n = 20000
-    k = rng.integers(0, 300, n).astype(np.uint64) * np.uint64(0x1234567)  # repeats, skeys below SKEY_LIMIT
+    k = _skeys(rng, 300)[rng.integers(0, 300, n)].astype(np.uint64)  # repeats
     vs = rng.integers(-64, 65, n).astype(np.int64)
     tl = rng.integers(0, 129, n).astype(np.uint64)
     w = np.ascontiguousarray(((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)) | k)

@@ -11,7 +11,7 @@ import torch
 
 import oracle
 from subproc_amd import _lib
-from subproc_amd.td import _SKEY_REGIONS, SKEY_LIMIT, skeys_to_keys
+from subproc_amd.td import skeys_to_keys
 
 pytestmark = pytest.mark.gpu
 
@@ -97,13 +97,14 @@ def sort_pair(keys, vals, keys_out, vals_out, n):
 
 
 def _skeys(rng, size):
-    """Random valid OTH_TD_SKEY values (td.py): any integer below SKEY_LIMIT
-    whose (discs, moves) pair is not (0, 64), which OTH_TD_KEY cannot hold;
-    the first and last valid ones included."""
-    s = rng.integers(0, SKEY_LIMIT - _SKEY_REGIONS, size=size, dtype=np.int64)
-    s[s >= 64 * _SKEY_REGIONS] += _SKEY_REGIONS  # skip pair 64 = (0, 64)
+    """Random OTH_TD_SKEY values (include/othello.h): (pair, region a) << 22 |
+    the regions b..h in their mixed radix, pair (discs, moves) 64 = (0, 64)
+    left out (OTH_TD_KEY cannot hold it); the first and last skeys included."""
+    hi = rng.integers(0, 2144 * 5, size=size, dtype=np.int64)
+    hi[hi >= 64 * 5] += 5
+    s = (hi << 22) | rng.integers(0, 4027725, size=size, dtype=np.int64)
     if size > 1:
-        s[0], s[-1] = 0, SKEY_LIMIT - 1
+        s[0], s[-1] = 0, ((2145 * 5 - 1) << 22) | (4027725 - 1)
     return s
 
 
@@ -470,7 +471,7 @@ def test_td_segments_words_pair():
     lam = np.array([0.9 ** j for j in range(129)], np.float64)
     for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 1023, 1024, 1025, 5000],
                                                                           400)):
-        keys = np.repeat(np.cumsum(rng.integers(1, 1 << 20, len(lens))).astype(np.uint64), lens)  # sorted skeys
+        keys = np.repeat(np.sort(_skeys(rng, len(lens))).astype(np.uint64), lens)  # sorted skeys
         n = len(keys)
         vs = rng.integers(-64, 65, n).astype(np.int64)
         tl = rng.integers(0, 129, n).astype(np.uint64)

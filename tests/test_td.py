@@ -171,7 +171,7 @@ def test_skey_order_and_round_trip():
     """include/othello.h OTH_TD_SKEY (the packed words' 36-bit sort key): a
     bijection on counts() tuples with moves <= 64 - discs that orders them as
     OTH_TD_KEY does, decoded alike by the scalar and the vectorised helper;
-    every value below SKEY_LIMIT fits 36 bits."""
+    every skey fits 36 bits."""
     rng = np.random.default_rng(5)
     cs = [(0,) * 10, (64, 0, 4, 8, 4, 8, 8, 16, 4, 12), (0, 63, 4, 8, 4, 8, 8, 16, 4, 12), (1, 63) + (0,) * 8]
     for _ in range(5000):
@@ -182,6 +182,6 @@ def test_skey_order_and_round_trip():
     assert all(td.skey_to_counts(s) == tuple(c) for s, c in zip(skeys, cs))
     np.testing.assert_array_equal(np.argsort(keys, kind="stable"), np.argsort(skeys, kind="stable"))
     np.testing.assert_array_equal(td.skeys_to_keys(skeys), keys)
-    assert td.SKEY_LIMIT <= 1 << _lib.TD_SKEY_BITS and skeys.max() == td.SKEY_LIMIT - 1
+    assert skeys.max() == td.counts_to_skey(cs[1]) < td.SKEY_LIMIT <= 1 << _lib.TD_SKEY_BITS
     with pytest.raises(ValueError):
         td.counts_to_skey((10, 55) + (0,) * 8)

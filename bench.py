@@ -680,8 +680,7 @@ def _bench_td(ops, torch, dev, args, games=1 << 18, reps=7):
           for k in range(3)]
     sm = StateMap(dev)
     for r in rs[:2]:  # the empty-table path, then the merge path (first-use kernel loading)
-        pk = ops.replay_rows(r.moves, r.plies)
-        sm.update(pk.boards, r.plies, pk.row_off)
+        sm.update_rows(ops.replay_rows(r.moves, r.plies), r.plies)
     base_k, base_v = sm.keys.clone(), sm.values.clone()
     r2 = rs[2]
     times, n_upd = [], 0
@@ -691,8 +690,7 @@ def _bench_td(ops, torch, dev, args, games=1 << 18, reps=7):
         t0 = time.perf_counter()
         # the books as GameBooks holds them: the packed replay (each game's
         # recorded rows only), then the update over those rows
-        pk = ops.replay_rows(r2.moves, r2.plies)
-        n_upd = sm.update(pk.boards, r2.plies, pk.row_off)
+        n_upd = sm.update_rows(ops.replay_rows(r2.moves, r2.plies), r2.plies)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     times = times[1:]

@@ -191,18 +191,37 @@ class StateMap:
         cnt = 2 * (plies.long().clamp(max=POS_STRIDE - 1) + 1)
         ends = torch.cumsum(cnt, 0)
         base = (ends - cnt).contiguous()
-        total = int(ends[-1])
+        return self._update_packed(pos_boards, plies, row_off, base, int(ends[-1]))
+
+    def update_rows(self, rows, plies):
+        """update() over the packed rows of ops.replay_rows(moves, plies) (a
+        ReplayRows: game g's rows start at row_off[g], the games' rows
+        contiguous and in order, min(plies, 128) + 1 each): the update
+        offsets are twice the row offsets and the total twice the row count,
+        so no device-to-host read precedes the update kernel (round 5)."""
+        n = plies.shape[0]
+        b, off = rows.boards, rows.row_off
+        if b.dim() != 2 or b.shape[1] != 2 or b.dtype != torch.int64 or off.shape != (n,) or \
+                off.dtype != torch.int64 or plies.dtype != torch.uint8 or \
+                not (b.device == off.device == plies.device == self.device):
+            raise ValueError("rows: ops.replay_rows of these plies on the map's device")
+        if n == 0:
+            return 0
+        return self._update_packed(b, plies, off, (2 * off).contiguous(), 2 * b.shape[0])
+
+    def _update_packed(self, pos_boards, plies, row_off, base, total):
+        n = plies.shape[0]
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            # the update stream as packed words (key | value_side | turn_left):
+            # the update stream as packed words (skey | turn_left | value_side):
             # half the bytes of (key, value) pairs through the sort
             words = torch.empty(total, dtype=torch.int64, device=self.device)
             check(lib.oth_td_updates_packed(pos_boards.contiguous().data_ptr(),
                                             None if row_off is None else row_off.contiguous().data_ptr(),
                                             plies.contiguous().data_ptr(), base.data_ptr(), words.data_ptr(), n,
                                             stream), "oth_td_updates_packed")
-            # a keys-only sort of the words by their key bits (the payload rides
+            # a keys-only sort of the words by their skey bits (the payload rides
             # along), then the segments straight from the sorted words, which
             # also writes each update's value (oth_td_segments_words: no
             # separate unpack into a keys array and a values array)
@@ -355,7 +374,7 @@ class StateMap:
 
     def update_from_books(self, books):
         """Apply a subproc_amd.books.GameBooks batch."""
-        return self.update(books.pos.boards, books.plies, books.pos.row_off)
+        return self.update_rows(books.pos, books.plies)
 
     def get(self, counts):
         """Value for a counts() tuple, 0.0 if absent (a fresh key reads as 0, 53-56)."""

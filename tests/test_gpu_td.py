@@ -32,6 +32,9 @@ def test_state_map_matches_reference_fixture_and_batches_compose():
     pk = ops.replay_rows(moves, plies)
     assert sm3.update(pk.boards, plies, pk.row_off) == int(2 * (z["plies"].astype(np.int64) + 1).sum())
     assert sm3.items() == want
+    sm5 = td.StateMap(DEV)  # round 5: offsets from the replay's own row offsets, no host read
+    assert sm5.update_rows(pk, plies) == int(2 * (z["plies"].astype(np.int64) + 1).sum())
+    assert sm5.items() == want
     from subproc_amd.books import GameBooks
     sm4 = td.StateMap(DEV)
     sm4.update_from_books(GameBooks(moves, plies))
@@ -55,6 +58,10 @@ def test_state_map_at_scale_vs_oracle():
     got = {td.key_to_counts(k): v for k, v in zip(sm.keys.cpu().tolist(), sm.values.cpu().tolist())}
     assert got == store
     assert torch.all(sm.keys[1:] > sm.keys[:-1])  # table stays sorted and unique
+    sm2 = td.StateMap(DEV)  # the packed rows (StateMap.update_rows), bit for bit the same table
+    for r in (r1, r2):
+        sm2.update_rows(ops.replay_rows(r.moves, r.plies), r.plies)
+    assert torch.equal(sm2.keys, sm.keys) and torch.equal(sm2.values.view(torch.int64), sm.values.view(torch.int64))
 
 
 @pytest.mark.parametrize("long_min,spec_warm", [(None, None), (48, None), (1024, None), (48, "1"), (1024, "3")])

@@ -26,8 +26,7 @@ for k in range(reps):
     r = ops.rollout(games, 0x5EED, (1 << 41) + k * games, "random", record_moves=True, device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pk = ops.replay_rows(r.moves, r.plies)
-    n = sm.update(pk.boards, r.plies, pk.row_off)
+    n = sm.update_rows(ops.replay_rows(r.moves, r.plies), r.plies)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print("batch %d: %d updates, %d keys, %.2f ms, %.3e updates/s" % (k, n, len(sm), dt * 1e3, n / dt), flush=True)

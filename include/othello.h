@@ -317,15 +317,6 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
                      int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream);
-/* oth_td_ema_split over the skey-sorted packed words (round 5): update i's
- * value is value_side * lam_pow[turn_left] of words[i] (oth_td_unpack's rule,
- * the same double), read where the EMA needs it, so no values array is
- * written between the segments and the EMA.  lam_pow: OTH_POS_STRIDE doubles
- * (device).  Same results as oth_td_ema_split over oth_td_unpack's values. */
-int oth_td_ema_split_words(const uint64_t* words, const double* lam_pow, const int64_t* seg_off, const double* init,
-                           double a, double one_minus_a, double* out, int64_t n_seg, int64_t long_min,
-                           const int64_t* long_idx, int64_t n_long, int64_t n_values, void* temp,
-                           size_t* temp_bytes, void* stream);
 
 /* Packed updates (the GPU books' path, StateMap.update): the update stream
  * of oth_td_updates / oth_td_updates_rows (row_off NULL: the strided table)
@@ -382,11 +373,8 @@ int oth_td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* s
 /* oth_td_segments over the skey-sorted packed words themselves (each read as
  * its low OTH_TD_SKEY_BITS; ukeys receives OTH_TD_KEY values), also
  * writing values[i] = value_side * lam_pow[turn_left] of word i
- * (oth_td_unpack's rule), so a sorted word stream needs no unpack pass: the
- * keys array oth_td_segments reads is never formed (round 5).  values: n
- * doubles (device), or NULL (the runs only: oth_td_ema_split_words reads the
- * words themselves; lam_pow may then be NULL too); the rest as
- * oth_td_segments. */
+ * (oth_td_unpack's rule), so a sorted word stream needs no unpack pass: the keys array oth_td_segments reads is never
+ * formed (round 5).  values: n doubles (device); the rest as oth_td_segments. */
 int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t n, int64_t long_min, int64_t* seg_off,
                           int64_t* ukeys, int64_t* long_idx, int64_t* counts, double* values, void* temp,
                           size_t* temp_bytes, void* stream);

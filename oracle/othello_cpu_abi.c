@@ -381,29 +381,6 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     return oth_td_ema(values, seg_off, init, a, one_minus_a, out, n_seg, stream);
 }
 
-/* the words' values by oth_td_unpack's rule into temp (n_values doubles),
- * then the EMA */
-int oth_td_ema_split_words(const uint64_t* words, const double* lam_pow, const int64_t* seg_off, const double* init,
-                           double a, double one_minus_a, double* out, int64_t n_seg, int64_t long_min,
-                           const int64_t* long_idx, int64_t n_long, int64_t n_values, void* temp,
-                           size_t* temp_bytes, void* stream) {
-    if (long_min < 1 || n_long < 0 || n_values < 0 || !temp_bytes || (n_long > 0 && !long_idx)) return OTH_EINVAL;
-    const size_t need = (size_t)(n_values > 0 ? n_values : 1) * sizeof(double);
-    if (!temp) {
-        *temp_bytes = need;
-        return OTH_OK;
-    }
-    if (*temp_bytes < need || (n_seg > 0 && (!words || !lam_pow || !seg_off))) return OTH_EINVAL;
-    if (n_seg <= 0) return oth_td_ema(NULL, seg_off, init, a, one_minus_a, out, n_seg, stream);
-    const int64_t nv = seg_off[n_seg];
-    if (nv > n_values) return OTH_EINVAL;
-    double* vals = (double*)temp;
-    for (int64_t i = 0; i < nv; i++)
-        vals[i] = (double)((int)(words[i] >> OTH_TD_PACK_VALUE_SHIFT) - 64) *
-                  lam_pow[(words[i] >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
-    return oth_td_ema(vals, seg_off, init, a, one_minus_a, out, n_seg, stream);
-}
-
 int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, void* temp, size_t* temp_bytes,
                       void* stream) {
     (void)stream;
@@ -458,16 +435,11 @@ int oth_td_segments_words(const uint64_t* words, const double* lam_pow, int64_t 
         *temp_bytes = need;
         return OTH_OK;
     }
-    if (*temp_bytes < need || !seg_off || !counts || (n > 0 && (!words || !ukeys || !long_idx || (values && !lam_pow))))
+    if (*temp_bytes < need || !seg_off || !counts || (n > 0 && (!words || !lam_pow || !ukeys || !long_idx || !values)))
         return OTH_EINVAL;
     int64_t* keys = (int64_t*)temp;
     size_t none = 0;
-    int rc = OTH_OK;
-    if (values) {
-        rc = oth_td_unpack(words, lam_pow, keys, values, n, stream);
-    } else { /* the runs only */
-        for (int64_t i = 0; i < n; i++) keys[i] = td_key_of_skey(words[i] & ((1ull << OTH_TD_SKEY_BITS) - 1));
-    }
+    int rc = oth_td_unpack(words, lam_pow, keys, values, n, stream);
     if (rc == OTH_OK) rc = oth_td_segments(keys, n, long_min, seg_off, ukeys, long_idx, counts, keys, &none, stream);
     return rc;
 }

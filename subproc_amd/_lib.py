@@ -55,8 +55,6 @@ SIGNATURES = {
     "oth_td_segments_words": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "oth_td_ema_split": (_I, [_P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64, _I64, _P, _P,
                               _P]),
-    "oth_td_ema_split_words": (_I, [_P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I64, _I64, _P, _I64,
-                                    _I64, _P, _P, _P]),
     "oth_td_sort_pairs": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),
     "oth_rollout_grid": (_I, [_I, _I64]),
     "oth_td_updates_packed": (_I, [_P, _P, _P, _P, _P, _I64, _P]),

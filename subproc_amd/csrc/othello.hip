@@ -1634,32 +1634,9 @@ __device__ __forceinline__ double td_step(double v, double x, double a, double o
 #pragma clang fp contract(off)
     return (v == 0.0) ? x : v * oma + x * a;
 }
-// The update values an EMA kernel reads: a values array, or (round 5) the
-// key-sorted packed words themselves, each value recomputed as oth_td_unpack
-// does (value_side * lam_pow[turn_left], the same double), lam_pow staged in
-// the kernel's LDS -- so the segments pass need not write a values array.
-struct TdVals {
-    const double* v;   // the values, or nullptr
-    const u64* w;      // the packed words (v == nullptr)
-    const double* lam; // lam_pow in LDS (words)
-    __device__ __forceinline__ double word_value(u64 x) const {
-        return (double)((int)(x >> OTH_TD_PACK_VALUE_SHIFT) - 64) *
-               lam[(x >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
-    }
-    __device__ __forceinline__ double at(int64_t i) const { return v ? v[i] : word_value(w[i]); }
-    __device__ __forceinline__ TdVals from(int64_t b) const { return TdVals{v ? v + b : nullptr, v ? nullptr : w + b, lam}; }
-};
-// (every thread of the block, before any returns)
-__device__ __forceinline__ TdVals td_vals(const double* vals, const u64* words, const double* lam_pow,
-                                          double* lam_s) {
-    if (!vals)
-        for (int k = threadIdx.x; k < OTH_POS_STRIDE; k += blockDim.x) lam_s[k] = lam_pow[k];
-    __syncthreads();
-    return TdVals{vals, vals ? nullptr : words, lam_s};
-}
-__device__ __forceinline__ void td_load(double (&b)[kTdChunk], const TdVals& src, int64_t i, int64_t last) {
+__device__ __forceinline__ void td_load(double (&b)[kTdChunk], const double* vals, int64_t i, int64_t last) {
 #pragma unroll
-    for (int k = 0; k < kTdChunk; k++) b[k] = src.at(min(i + k, last));  // clamped: always in bounds
+    for (int k = 0; k < kTdChunk; k++) b[k] = vals[min(i + k, last)];  // clamped: always in bounds
 }
 __device__ __forceinline__ double td_run(double v, const double (&b)[kTdChunk], int m, double a, double oma) {
 #pragma unroll
@@ -1695,10 +1672,10 @@ __device__ __forceinline__ double td_run_full(double v, const double (&b)[kTdChu
 // the rule over vals[i, e) from state v, one thread: short ranges step by
 // step; long ones software-pipelined (a ring of three chunks keeps 2 * kTdChunk
 // loads in flight while the chain consumes the third)
-__device__ __forceinline__ double td_range(double v, const TdVals& vals, int64_t i, const int64_t e, double a,
-                                          double oma) {
+__device__ __forceinline__ double td_range(double v, const double* __restrict__ vals, int64_t i, const int64_t e, double a,
+                           double oma) {
     if (e - i < 3 * kTdChunk) {  // the common case: a handful of updates
-        for (; i < e; i++) v = td_step(v, vals.at(i), a, oma);
+        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
         return v;
     }
     const int64_t last = e - 1;
@@ -1725,14 +1702,10 @@ __device__ __forceinline__ double td_range(double v, const TdVals& vals, int64_t
 // so the kernel has no ring of loads and needs a fraction of the registers:
 // more waves in flight for the millions of 1- to 3-update keys.
 template <bool SHORT>
-__global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ values,
-                                                        const u64* __restrict__ words,
-                                                        const double* __restrict__ lam_pow,
+__global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
                                                         const int64_t* __restrict__ seg_off,
                                                         const double* __restrict__ init, double a, double oma,
                                                         double* __restrict__ out, int64_t n_seg, int64_t long_min) {
-    __shared__ double lam_s[OTH_POS_STRIDE];
-    const TdVals vals = td_vals(values, words, lam_pow, lam_s);
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= n_seg) return;
     int64_t i = seg_off[s];
@@ -1740,7 +1713,7 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
     if (long_min > 0 && e - i >= long_min) return;
     double v = init ? init[s] : 0.0;
     if (SHORT) {
-        for (; i < e; i++) v = td_step(v, vals.at(i), a, oma);
+        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
         out[s] = v;
     } else {
         out[s] = td_range(v, vals, i, e, a, oma);
@@ -1813,7 +1786,7 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // the wave streams [ws, j) of the key's values kv[0, n) from state v (live
 // lanes only; ws and j relative to kv), recording in g its state at i (a
 // round boundary at or after ws).  kv and n wave-uniform.
-__device__ __forceinline__ void spec_stream(const TdVals& kv, int n, bool live, int ws, int i, int j, double& v,
+__device__ __forceinline__ void spec_stream(const double* kv, int n, bool live, int ws, int i, int j, double& v,
                                             double& g, double a, double oma, SpecWave& sh) {
     const int p = threadIdx.x;
     const int rounds_p = live ? (j - ws + kTdChunk - 1) / kTdChunk : 0;
@@ -1828,22 +1801,20 @@ __device__ __forceinline__ void spec_stream(const TdVals& kv, int n, bool live, 
     int off[kTdChunk];
 #pragma unroll
     for (int k = 0; k < kTdChunk; k++) off[k] = (sh.start[k * kSpecRowsPerLoad + (p >> 4)] + (p & 15)) * 8;
-    // (raw 64-bit loads: values, or packed words converted as they are parked)
-    auto fetch = [&](u64(&r)[kTdChunk], int round) {
+    auto fetch = [&](double(&r)[kTdChunk], int round) {
         const int base = round * kTdChunk;
-        void* const at = kv.v ? (void*)(kv.v + base) : (void*)(kv.w + base);
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(at, (short)0, max(n - base, 0) * 8, 0x00020000);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(kv + base), (short)0, max(n - base, 0) * 8,
+                                                            0x00020000);
 #pragma unroll
         for (int k = 0; k < kTdChunk; k++)
-            r[k] = __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off[k], 0, 0));
+            r[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off[k], 0, 0));
     };
-    auto park = [&](const u64(&r)[kTdChunk], int buf) {
+    auto park = [&](const double(&r)[kTdChunk], int buf) {
 #pragma unroll
         for (int k = 0; k < kTdChunk; k++)
-            sh.stage[buf][(k * kSpecRowsPerLoad + (p >> 4)) * kSpecRow + (p & 15)] =
-                kv.v ? __builtin_bit_cast(double, r[k]) : kv.word_value(r[k]);
+            sh.stage[buf][(k * kSpecRowsPerLoad + (p >> 4)) * kSpecRow + (p & 15)] = r[k];
     };
-    u64 rg[kSpecAhead][kTdChunk];
+    double rg[kSpecAhead][kTdChunk];
 #pragma unroll
     for (int u = 0; u < kSpecAhead; u++) fetch(rg[u], u);
     for (int r0 = 0; r0 < rounds; r0 += kSpecAhead) {
@@ -1945,9 +1916,7 @@ __device__ __forceinline__ int64_t spec_key_of(const SpecPlanEntry* plan, int64_
     return lo;
 }
 // one wave per work item: parts q = 64 c + lane of its key, guesses and end states out
-__global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double* __restrict__ values,
-                                                                   const u64* __restrict__ words,
-                                                                   const double* __restrict__ lam_pow,
+__global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double* __restrict__ vals,
                                                                    const int64_t* __restrict__ seg_off,
                                                                    const double* __restrict__ init, double a,
                                                                    double oma, const int64_t* __restrict__ hdr,
@@ -1955,8 +1924,6 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double*
                                                                    double* __restrict__ guess,
                                                                    double* __restrict__ fin, int warm16) {
     __shared__ SpecWave sh;
-    __shared__ double lam_s[OTH_POS_STRIDE];
-    const TdVals vals = td_vals(values, words, lam_pow, lam_s);
     const int64_t n_spec = uniform64(hdr[0]), items = uniform64(hdr[1]);
     for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
         const int64_t key = uniform64(spec_key_of(plan, n_spec, w));
@@ -1968,7 +1935,7 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double*
         const bool live = q < np;
         const int i = (int)q * kSpecLen, j = live ? min(i + kSpecLen, n) : i, ws = max(0, i - warm16);
         double v = (ws == 0 && init) ? init[s] : 0.0, g = v;
-        spec_stream(vals.from(b), n, live, ws, i, j, v, g, a, oma, sh);
+        spec_stream(vals + b, n, live, ws, i, j, v, g, a, oma, sh);
         if (live) {
             guess[pb + q] = g;
             fin[pb + q] = v;
@@ -1977,9 +1944,7 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double*
 }
 // one wave per split key: its parts checked in order, 64 at a time; missed
 // guesses rerun from their predecessor's end state until all match
-__global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* __restrict__ values,
-                                                                 const u64* __restrict__ words,
-                                                                 const double* __restrict__ lam_pow,
+__global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* __restrict__ vals,
                                                                  const int64_t* __restrict__ seg_off,
                                                                  const double* __restrict__ init, double a,
                                                                  double oma, const int64_t* __restrict__ hdr,
@@ -1988,8 +1953,6 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* _
                                                                  const double* __restrict__ fin,
                                                                  double* __restrict__ out) {
     __shared__ SpecWave sh;
-    __shared__ double lam_s[OTH_POS_STRIDE];
-    const TdVals vals = td_vals(values, words, lam_pow, lam_s);
     const int lane = threadIdx.x;
     const int64_t n_spec = uniform64(hdr[0]);
     for (int64_t key = blockIdx.x; key < n_spec; key += gridDim.x) {
@@ -1999,7 +1962,7 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* _
         const int n = (int)uniform64(seg_off[s + 1] - b);
         if (np == 0) {  // parts past the scratch (td_spec_plan_kernel): the whole key on lane 0
             double v = init ? init[s] : 0.0, unused = v;
-            spec_stream(vals.from(b), n, lane == 0, 0, 0, n, v, unused, a, oma, sh);
+            spec_stream(vals + b, n, lane == 0, 0, 0, n, v, unused, a, oma, sh);
             if (lane == 0) out[s] = v;
             continue;
         }
@@ -2015,7 +1978,7 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_fix_kernel(const double* _
                 if (!__ballot(miss)) break;  // wave-uniform
                 const int i = (int)q * kSpecLen, j = miss ? min(i + kSpecLen, n) : i;
                 double w = pred, unused = pred;
-                spec_stream(vals.from(b), n, miss, i, i, j, w, unused, a, oma, sh);
+                spec_stream(vals + b, n, miss, i, i, j, w, unused, a, oma, sh);
                 if (miss) {
                     g = pred;
                     f = w;
@@ -2040,9 +2003,7 @@ inline size_t spec_scratch_bytes(int64_t n_long, int64_t n_values) {
 // from LDS while the next stage is in flight, so the time is the chain's.
 constexpr int kTdStage = 1024;                 // doubles per LDS stage
 constexpr int kTdStageLoads = kTdStage / 64;   // loads per lane per stage
-__global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ values,
-                                                         const u64* __restrict__ words,
-                                                         const double* __restrict__ lam_pow,
+__global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ vals,
                                                          const int64_t* __restrict__ seg_off,
                                                          const double* __restrict__ init, double a, double oma,
                                                          double* __restrict__ out,
@@ -2050,8 +2011,6 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
     // (ystage rows padded by one chunk: the chain prefetches the next chunk's y
     // unconditionally)
     __shared__ double stage[2][kTdStage], ystage[2][kTdStage + kTdChunk];
-    __shared__ double lam_s[OTH_POS_STRIDE];
-    const TdVals vals = td_vals(values, words, lam_pow, lam_s);
     const int lane = threadIdx.x;
     const int64_t s = long_idx[blockIdx.x];
     const int64_t b = seg_off[s], e = seg_off[s + 1];
@@ -2062,7 +2021,7 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
 #pragma unroll
         for (int k = 0; k < kTdStageLoads; k++) {
             const int64_t idx = b + c * kTdStage + k * 64 + lane;
-            r[k] = idx < e ? vals.at(idx) : 0.0;
+            r[k] = idx < e ? vals[idx] : 0.0;
         }
     };
     auto park = [&](int buf) {
@@ -2478,8 +2437,8 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
                double* out, int64_t n_seg, void* stream) {
     if (n_seg < 0 || (n_seg > 0 && (!values || !seg_off || !out))) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
-    td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, nullptr, nullptr, seg_off,
-                                                                                init, a, one_minus_a, out, n_seg, 0);
+    td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                one_minus_a, out, n_seg, 0);
     return launched();
 }
 
@@ -2500,16 +2459,11 @@ static int64_t td_spec_warm(double oma) {
     return w > (double)(1 << 20) ? 0 : (int64_t)w;
 }
 
-}  // extern "C"
-namespace {
-// oth_td_ema_split over values (words == nullptr) or over packed words
-int td_ema_split(const double* values, const u64* words, const double* lam_pow, const int64_t* seg_off,
-                 const double* init, double a, double one_minus_a, double* out, int64_t n_seg, int64_t long_min,
-                 const int64_t* long_idx, int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes,
-                 hipStream_t st) {
-    const bool have = words ? lam_pow != nullptr : values != nullptr;
+int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
+                     double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
+                     int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream) {
     if (n_seg < 0 || long_min < 1 || n_long < 0 || n_long > n_seg || n_values < 0 || !temp_bytes ||
-        (n_seg > 0 && (!have || !seg_off || !out)) || (n_long > 0 && !long_idx))
+        (n_seg > 0 && (!values || !seg_off || !out)) || (n_long > 0 && !long_idx))
         return OTH_EINVAL;
     const int64_t warm = td_spec_warm(one_minus_a);
     const size_t need = warm > 0 && n_long > 0 ? spec_scratch_bytes(n_long, n_values) : 0;
@@ -2519,17 +2473,16 @@ int td_ema_split(const double* values, const u64* words, const double* lam_pow, 
     }
     if (*temp_bytes < need) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
-    if (words) values = nullptr;
     if (long_min <= 3 * kTdChunk)
-        td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, st>>>(values, words, lam_pow, seg_off, init, a,
-                                                                  one_minus_a, out, n_seg, long_min);
+        td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                   one_minus_a, out, n_seg, long_min);
     else
-        td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, st>>>(values, words, lam_pow, seg_off, init, a,
-                                                                   one_minus_a, out, n_seg, long_min);
+        td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                    one_minus_a, out, n_seg, long_min);
     int rc = launched();
     if (rc != OTH_OK || n_long == 0) return rc;
-    td_ema_long_kernel<<<(unsigned)n_long, 64, 0, st>>>(values, words, lam_pow, seg_off, init, a, one_minus_a, out,
-                                                         long_idx, warm);
+    td_ema_long_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
+                                                                         out, long_idx, warm);
     rc = launched();
     if (rc != OTH_OK || warm <= 0) return rc;
     // the split keys: plan, parts (one wave per 64 parts), check and reruns
@@ -2539,41 +2492,24 @@ int td_ema_split(const double* values, const u64* words, const double* lam_pow, 
     const int64_t parts = n_values / kSpecLen + n_long + 1;
     double* fin = guess + parts;
     const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
-    const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, st);
+    const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, (hipStream_t)stream);
     if (me != hipSuccess) return status(me);
-    td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, st>>>(seg_off, long_idx, n_long, kSpecMinWarms * warm,
-                                                                  hdr, plan);
+    td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long,
+                                                                                    kSpecMinWarms * warm, hdr, plan);
     rc = launched();
     if (rc != OTH_OK) return rc;
-    td_spec_plan_kernel<<<1, 1024, 0, st>>>(hdr, plan, parts);
+    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan, parts);
     rc = launched();
     if (rc != OTH_OK) return rc;
     const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
-    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, st>>>(values, words, lam_pow, seg_off, init, a,
-                                                                  one_minus_a, hdr, plan, guess, fin, warm16);
+    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
+                                                                                   one_minus_a, hdr, plan, guess,
+                                                                                   fin, warm16);
     rc = launched();
     if (rc != OTH_OK) return rc;
-    td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, st>>>(
-        values, words, lam_pow, seg_off, init, a, one_minus_a, hdr, plan, guess, fin, out);
+    td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, (hipStream_t)stream>>>(
+        values, seg_off, init, a, one_minus_a, hdr, plan, guess, fin, out);
     return launched();
-}
-}  // namespace
-extern "C" {
-
-int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
-                     double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
-                     int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream) {
-    return td_ema_split(values, nullptr, nullptr, seg_off, init, a, one_minus_a, out, n_seg, long_min, long_idx,
-                        n_long, n_values, temp, temp_bytes, (hipStream_t)stream);
-}
-
-int oth_td_ema_split_words(const uint64_t* words, const double* lam_pow, const int64_t* seg_off, const double* init,
-                           double a, double one_minus_a, double* out, int64_t n_seg, int64_t long_min,
-                           const int64_t* long_idx, int64_t n_long, int64_t n_values, void* temp,
-                           size_t* temp_bytes, void* stream) {
-    if (!words && n_seg > 0) return OTH_EINVAL;
-    return td_ema_split(nullptr, reinterpret_cast<const u64*>(words), lam_pow, seg_off, init, a, one_minus_a, out,
-                        n_seg, long_min, long_idx, n_long, n_values, temp, temp_bytes, (hipStream_t)stream);
 }
 
 int oth_rollout_grid(int policy, int64_t n) {

@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
 #pragma unroll
     for (int r = 0; r < kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
-        if (WORDS && WRITE && values && i < n) {
+        if (WORDS && WRITE && i < n) {
             const int vs = (int)(payload[r] >> (OTH_TD_PACK_VALUE_SHIFT - OTH_TD_PACK_TURN_SHIFT)) - 64;
             values[i] = (double)vs * lam_pow[payload[r] & OTH_TD_PACK_TURN_MASK];
         }
@@ -1280,7 +1280,7 @@ int td_segments(const int64_t* keys, int64_t n, int64_t long_min, int64_t* seg_o
         return OTH_OK;
     }
     if (!seg_off || !counts || (n > 0 && (!keys || !ukeys || !long_idx)) || *temp_bytes < need) return OTH_EINVAL;
-    if (WORDS && n > 0 && values && !lam_pow) return OTH_EINVAL;  // (values NULL: runs only)
+    if (WORDS && n > 0 && (!lam_pow || !values)) return OTH_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     int64_t* wave_cnt = static_cast<int64_t*>(temp);
     int64_t* wave_off = wave_cnt + slots;

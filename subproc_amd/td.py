@@ -222,16 +222,17 @@ class StateMap:
                                             plies.contiguous().data_ptr(), base.data_ptr(), words.data_ptr(), n,
                                             stream), "oth_td_updates_packed")
             # a keys-only sort of the words by their skey bits (the payload rides
-            # along), then the segments straight from the sorted words
-            # (oth_td_segments_words) and the EMA reading each update's value
-            # from its word (oth_td_ema_split_words): no unpack into keys and
-            # values, no values array (round 5)
+            # along), then the segments straight from the sorted words, which
+            # also writes each update's value (oth_td_segments_words: no
+            # separate unpack into a keys array and a values array)
             sorted_words = torch.empty_like(words)
             _with_scratch(lib.oth_td_sort_packed, (words.data_ptr(), sorted_words.data_ptr(), total), stream,
                           self.device, "oth_td_sort_packed")
             del words
-            segs = self._segments(sorted_words, words=True)
-        self._apply_segments(sorted_words, *segs, words=True)
+            sv = torch.empty(total, dtype=torch.float64, device=self.device)
+            segs = self._segments(sorted_words, sv)
+            del sorted_words
+        self._apply_segments(sv, *segs)
         return total
 
     def update_from_records(self, books):
@@ -282,14 +283,14 @@ class StateMap:
         """The key-sorted update stream (equal keys in stream order) into the
         table: each key's EMA in stream order, then the merge."""
         with torch.cuda.device(self.device):
-            segs = self._segments(sk)
+            segs = self._segments(sk, None)
         self._apply_segments(sv, *segs)
 
-    def _segments(self, sorted_in, words=False):
+    def _segments(self, sorted_in, values):
         """The sorted stream's segments in one pass pair and one host sync:
-        from keys (oth_td_segments) or from the sorted packed words
-        (oth_td_segments_words, no values written).  Returns (ukeys, seg_off,
-        long_idx)."""
+        from keys (oth_td_segments), or (values given) from the sorted packed
+        words, the values written as a side effect (oth_td_segments_words).
+        Returns (ukeys, seg_off, long_idx)."""
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         n = sorted_in.numel()
@@ -297,20 +298,20 @@ class StateMap:
         ukeys = torch.empty(n, dtype=torch.int64, device=self.device)
         long_idx = torch.empty(n, dtype=torch.int64, device=self.device)
         cnt = torch.empty(2, dtype=torch.int64, device=self.device)
-        if not words:
+        if values is None:
             _with_scratch(lib.oth_td_segments, (sorted_in.data_ptr(), n, LONG_MIN, seg_off.data_ptr(),
                                                 ukeys.data_ptr(), long_idx.data_ptr(), cnt.data_ptr()), stream,
                           self.device, "oth_td_segments")
         else:
-            _with_scratch(lib.oth_td_segments_words, (sorted_in.data_ptr(), None, n, LONG_MIN, seg_off.data_ptr(),
-                                                      ukeys.data_ptr(), long_idx.data_ptr(), cnt.data_ptr(), None),
-                          stream, self.device, "oth_td_segments_words")
+            _with_scratch(lib.oth_td_segments_words, (sorted_in.data_ptr(), self._lam_pow.data_ptr(), n, LONG_MIN,
+                                                      seg_off.data_ptr(), ukeys.data_ptr(), long_idx.data_ptr(),
+                                                      cnt.data_ptr(), values.data_ptr()), stream, self.device,
+                          "oth_td_segments_words")
         n_upd, n_long = cnt.tolist()
         return ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
 
-    def _apply_segments(self, sv, ukeys, seg_off, long_idx, words=False):
-        """Each key's EMA in stream order over its segment of sv (the values,
-        or the sorted packed words), then the merge."""
+    def _apply_segments(self, sv, ukeys, seg_off, long_idx):
+        """Each key's EMA in stream order over its segment of sv, then the merge."""
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
@@ -333,16 +334,10 @@ class StateMap:
             # keys with many updates (the opening and the first plies of every
             # game) are each run by a whole wavefront, the longest split into
             # parts over many (oth_td_ema_split)
-            if words:
-                _with_scratch(lib.oth_td_ema_split_words,
-                              (sv.data_ptr(), self._lam_pow.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a,
-                               1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN, long_idx.data_ptr(),
-                               long_idx.numel(), sv.numel()), stream, self.device, "oth_td_ema_split_words")
-            else:
-                _with_scratch(lib.oth_td_ema_split, (sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a,
-                                                     1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN,
-                                                     long_idx.data_ptr(), long_idx.numel(), sv.numel()),
-                              stream, self.device, "oth_td_ema_split")
+            _with_scratch(lib.oth_td_ema_split, (sv.data_ptr(), seg_off.data_ptr(), init.data_ptr(), self.a,
+                                                 1 - self.a, out.data_ptr(), ukeys.numel(), LONG_MIN,
+                                                 long_idx.data_ptr(), long_idx.numel(), sv.numel()),
+                          stream, self.device, "oth_td_ema_split")
             if pending is None:  # (a copy: ukeys is a view of an n-entry buffer)
                 self.keys, self.values = ukeys.clone(), out
             else:

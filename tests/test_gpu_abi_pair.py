@@ -432,28 +432,6 @@ def test_td_pair():
     both_scratch("oth_td_ema_split", sv, seg, init, 0.03, 1 - 0.03, out2, len(uk), 48, li, len(li.h), total)
     same(out2)
     np.testing.assert_array_equal(out2.h, out.h)
-    # round 5: the segments of the sorted words without a values array, and
-    # the EMA reading each value from its word (oth_td_ema_split_words)
-    off3, uk3, li3, cnt3 = (Buf(np.zeros(total + 1, np.int64)), Buf(np.zeros(total, np.int64)),
-                            Buf(np.zeros(total, np.int64)), Buf(np.zeros(2, np.int64)))
-    gpu, cpu = _lib.load(), oracle.cpu_abi()
-    st = torch.cuda.current_stream().cuda_stream
-    for lib, ptr, s in ((cpu, lambda b: HOSTP(b.h), None), (gpu, lambda b: b.d.data_ptr(), st)):
-        tb = ctypes.c_size_t(0)
-        args = (ptr(sw), None, total, 48, ptr(off3), ptr(uk3), ptr(li3), ptr(cnt3), None)
-        assert lib.oth_td_segments_words(*args, None, ctypes.byref(tb), s) == 0
-        temp = (torch.empty(max(tb.value, 1), dtype=torch.uint8, device=DEV) if lib is gpu
-                else np.zeros(max(tb.value, 1), np.uint8))
-        assert lib.oth_td_segments_words(*args, temp.data_ptr() if lib is gpu else HOSTP(temp), ctypes.byref(tb),
-                                         s) == 0
-        torch.cuda.synchronize()
-        m = int((cnt3.d.cpu().numpy() if lib is gpu else cnt3.h)[0])
-        np.testing.assert_array_equal((off3.d.cpu().numpy() if lib is gpu else off3.h)[:m + 1], seg.h)
-        np.testing.assert_array_equal((uk3.d.cpu().numpy() if lib is gpu else uk3.h)[:m], uk)
-    out3 = Buf(np.zeros(len(uk), np.float64))
-    both_scratch("oth_td_ema_split_words", sw, lam, seg, init, 0.03, 1 - 0.03, out3, len(uk), 48, li, len(li.h), total)
-    same(out3)
-    np.testing.assert_array_equal(out3.h.view(np.int64), out.h.view(np.int64))
 
 
 def test_td_segments_pair():

@@ -154,39 +154,6 @@ def test_td_ema_split_speculation_learner_rate(kind, short):
     assert out.cpu().tolist() == want
 
 
-@pytest.mark.parametrize("kind", ["normal", "sparse"])
-def test_td_ema_split_words_equals_values(kind):
-    """oth_td_ema_split_words (round 5: each value read from its packed word,
-    value_side * lam_pow[turn_left]) equals oth_td_ema_split over the same
-    words unpacked (oth_td_unpack), bit for bit, on short, wave-long and split
-    keys (sparse: mostly value 0, so exact zero states and restarts)."""
-    from subproc_amd import _lib
-    lib = _lib.load()
-    st = torch.cuda.current_stream().cuda_stream
-    rng = np.random.default_rng(21 if kind == "normal" else 22)
-    lengths = np.concatenate([rng.integers(1, 5, 5000), [47, 48, 49, 1023, 1024, 1025, 5825, 5826, 9000, 70001]])
-    n = int(lengths.sum())
-    vs = rng.integers(-64, 65, n) if kind == "normal" else np.where(rng.random(n) < 0.8, 0, rng.integers(-64, 65, n))
-    tl = rng.integers(0, 129, n).astype(np.uint64)
-    sk = np.repeat(np.arange(len(lengths), dtype=np.uint64) * np.uint64(1 << 22), lengths)
-    w = torch.from_numpy(((vs + 64).astype(np.uint64) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT))
-                         | sk).to(DEV)
-    lam = torch.tensor(td.lam_pow_table(), dtype=torch.float64, device=DEV)
-    keys = torch.empty(n, dtype=torch.int64, device=DEV)
-    vals = torch.empty(n, dtype=torch.float64, device=DEV)
-    _lib.check(lib.oth_td_unpack(w.data_ptr(), lam.data_ptr(), keys.data_ptr(), vals.data_ptr(), n, st), "unpack")
-    seg = torch.from_numpy(np.r_[0, np.cumsum(lengths)].astype(np.int64)).to(DEV)
-    init = torch.from_numpy(rng.choice([0.0, 0.5, -1.25], len(lengths))).to(DEV)
-    li = torch.from_numpy(np.flatnonzero(lengths >= 48).astype(np.int64)).to(DEV)
-    outs = []
-    for fn, src in ((lib.oth_td_ema_split, (vals.data_ptr(),)), (lib.oth_td_ema_split_words, (w.data_ptr(), lam.data_ptr()))):
-        out = torch.empty(len(lengths), dtype=torch.float64, device=DEV)
-        td._with_scratch(fn, (*src, seg.data_ptr(), init.data_ptr(), td.A, 1 - td.A, out.data_ptr(), len(lengths), 48,
-                              li.data_ptr(), li.numel(), n), st, DEV, "ema")
-        outs.append(out.view(torch.int64).cpu())
-    assert torch.equal(outs[0], outs[1])
-
-
 def test_fit_on_device_matches_sklearn():
     from sklearn import linear_model
     from subproc_amd import params

@@ -702,6 +702,7 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     __shared__ int64_t sk[kMergeTile];
     __shared__ double sv[kMergeTile];
     __shared__ unsigned long long range[2];  // min slot, max slot + 1 of the block's outputs
+    __shared__ int64_t prev_s;               // the batch key before the tile's first
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kMergeTile;
     const int64_t d1 = d0 + kMergeTile < nA + nB ? d0 + kMergeTile : nA + nB;
@@ -713,6 +714,7 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     const int64_t a0 = s0, b0 = d0 - a0;
     const int na = (int)(s1 - a0), nb = (int)(d1 - s1 - b0);
     const int n = na + nb;
+    if (tid == 0) prev_s = b0 > 0 ? B[b0 - 1] : -1;
     stage_tile<kMergeK>(A, Av, a0, na, B, Bv, b0, n, sk, sv);
     __syncthreads();
     const int t0 = min(tid * kMergeK, n), t1 = min(t0 + kMergeK, n);
@@ -723,7 +725,10 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
         else hi = mid;
     }
     int i = lo, j = t0 - lo;
-    int64_t prev_b = t0 < t1 && b0 + j > 0 ? B[b0 + j - 1] : -1;  // keys are >= 0: -1 matches none
+    // the batch key before this thread's first (keys are >= 0: -1 matches
+    // none): from LDS, the tile's first from prev_s (round 5: a global load
+    // per thread on the merge's critical path)
+    int64_t prev_b = t0 < t1 ? (j > 0 ? sk[na + j - 1] : prev_s) : -1;
     // (a caller's inconsistent new_before must not send a store out of bounds)
     const uint64_t n_out = (uint64_t)(nA + new_before[nB]);
     int64_t ok[kMergeK];

@@ -739,27 +739,32 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     // the merge walk first, recording each output's batch index; then the
     // new_before loads of all of them at once (in the walk they were one
     // dependent global load per step; round 4)
+    // Branch-free (round 5: the branchy walk compiled to ~420 v_mov_b64 of
+    // predicated state copies): the two heads ka / kb stay in registers, a
+    // step takes the smaller (A only if strictly smaller: a batch key before
+    // its table copy), reads the taken element's value and refills the taken
+    // head from LDS.  Heads past their side read as INT64_MAX (keys are
+    // below 2^43).
     int64_t bq[kMergeK];
+    constexpr int64_t kEnd = INT64_MAX;
+    int64_t ka = i < na ? sk[i] : kEnd, kb = j < nb ? sk[na + j] : kEnd;
 #pragma unroll
     for (int q = 0; q < kMergeK; q++) {
-        bq[q] = -1;  // no output
-        const int m = t0 + q;
-        if (m >= t1) continue;
-        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
-            const int64_t key = sk[i];
-            if (key != prev_b) {  // not the table copy of the batch key just taken
-                bq[q] = b0 + j;
-                ok[q] = key;
-                ov[q] = sv[i];
-            }
-            i++;
-        } else {
-            const int64_t key = sk[na + j];
-            bq[q] = b0 + j;
-            ok[q] = key;
-            ov[q] = sv[na + j];
-            prev_b = key;
-            j++;
+        const bool valid = t0 + q < t1;
+        const bool takeA = ka < kb;  // (a valid step has a head below kEnd)
+        const int at = takeA ? i : na + j;
+        const int64_t key = takeA ? ka : kb;
+        ov[q] = sv[at];
+        ok[q] = key;
+        bq[q] = valid && !(takeA && key == prev_b) ? b0 + j : -1;  // a table copy of the batch key just taken: dropped
+        if (valid) {
+            prev_b = takeA ? prev_b : key;
+            i += takeA;
+            j += !takeA;
+            const int nx = takeA ? i : na + j;
+            const int64_t head = (takeA ? i < na : j < nb) ? sk[nx] : kEnd;
+            ka = takeA ? head : ka;
+            kb = takeA ? kb : head;
         }
     }
     int64_t nbq[kMergeK];
@@ -863,16 +868,25 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
         else hi = mid;
     }
     int i = lo, j = t0 - lo;
-    for (int m = t0; m < t1; m++) {
-        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
-            i++;
-            continue;
+    // branch-free walk, the two heads in registers (as td_merge_kernel)
+    constexpr int64_t kEnd = INT64_MAX;
+    int64_t ka = i < na ? sk[i] : kEnd, kb = j < nb ? sk[na + j] : kEnd;
+#pragma unroll
+    for (int q = 0; q < kLookupK; q++) {
+        if (t0 + q >= t1) break;
+        const bool takeA = ka < kb;
+        if (!takeA) {
+            // batch key b0 + j; the next table key is A[a0 + i] (past the tile: from HBM)
+            const int64_t ai = a0 + i;
+            const int64_t next = i < na ? ka : (ai < nA ? A[ai] : -1);
+            shit[j] = next == kb ? i : -1;
         }
-        // batch key b0 + j; the next table key is A[a0 + i] (past the tile: from HBM)
-        const int64_t key = sk[na + j], ai = a0 + i;
-        const int64_t next = i < na ? sk[i] : (ai < nA ? A[ai] : -1);
-        shit[j] = next == key ? i : -1;
-        j++;
+        i += takeA;
+        j += !takeA;
+        const int nx = takeA ? i : na + j;
+        const int64_t head = (takeA ? i < na : j < nb) ? sk[nx] : kEnd;
+        ka = takeA ? head : ka;
+        kb = takeA ? kb : head;
     }
     __syncthreads();
     // the hits' values loaded here, all in flight at once, not one per step of

@@ -1569,6 +1569,7 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
 #ifndef OTH_TD_UPD_WAVE
 #define OTH_TD_UPD_WAVE 1
 #endif
+template <bool WORDS>
 __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __restrict__ pos,
                                                                  const int64_t* __restrict__ row_off,
                                                                  const uint8_t* __restrict__ plies,
@@ -1587,7 +1588,7 @@ __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __re
     for (u32 p = lane; p <= np; p += 64) {
         const ulonglong2 b = row[p];
         const int64_t j = jb + 2 * (int64_t)(np - p);
-        if (words) {
+        if (WORDS) {
             const u64 t = (u64)(np - p) << OTH_TD_PACK_TURN_SHIFT;
             words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
             words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
@@ -2173,8 +2174,8 @@ inline int launched() { return status(hipGetLastError()); }
 static int td_updates_launch(const u64* pos, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                              const double* lam_pow, int64_t* keys, double* vals, u64* words, int64_t n, hipStream_t s) {
     if (OTH_TD_UPD_WAVE)
-        td_updates_wave_kernel<<<blocks_for(n * 64), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys, vals,
-                                                                     words, n);
+        (words ? td_updates_wave_kernel<true> : td_updates_wave_kernel<false>)<<<blocks_for(n * 64), kBlock, 0, s>>>(
+            pos, row_off, plies, base, lam_pow, keys, vals, words, n);
     else
         td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys,
                                                                              vals, words, n);

@@ -386,7 +386,10 @@ int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, voi
                       void* stream);
 
 /* Packed words -> keys[i] = the OTH_TD_KEY of the word's skey and values[i] =
- * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device). */
+ * value_side * lam_pow[turn_left] (lam_pow: OTH_POS_STRIDE doubles, device).
+ * Every entry point that reads a word's turn_left (this one,
+ * oth_td_sort_unpack, oth_td_segments_words) clamps it to OTH_POS_STRIDE - 1,
+ * so words not made by oth_td_updates_packed never read past lam_pow. */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                   void* stream);
 

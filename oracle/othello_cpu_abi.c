@@ -315,6 +315,12 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
     return OTH_OK;
 }
 
+/* turn_left as a lam_pow index, clamped to the table (as the GPU build) */
+static uint64_t td_turn_idx(uint64_t w) {
+    const uint64_t t = (w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK;
+    return t < OTH_POS_STRIDE - 1 ? t : OTH_POS_STRIDE - 1;
+}
+
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                   void* stream) {
     (void)stream;
@@ -322,7 +328,7 @@ int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, d
     for (int64_t i = 0; i < n; i++) {
         keys[i] = td_key_of_skey(words[i] & ((1ull << OTH_TD_SKEY_BITS) - 1));
         values[i] = (double)((int)(words[i] >> OTH_TD_PACK_VALUE_SHIFT) - 64) *
-                    lam_pow[(words[i] >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
+                    lam_pow[td_turn_idx(words[i])];
     }
     return OTH_OK;
 }

@@ -28,6 +28,13 @@
 #include "../../include/othello.h"
 #include "td_skey.hpp"
 
+// a packed word's turn_left as an index into lam_pow (OTH_POS_STRIDE
+// entries): clamped, so a word that did not come from oth_td_updates_packed
+// (turn_left above 128) cannot read past the table
+__device__ __forceinline__ uint32_t td_turn_idx(uint64_t w) {
+    return min((uint32_t)(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK, (uint32_t)OTH_POS_STRIDE - 1u);
+}
+
 namespace {
 
 // onesweep digit width, items per thread and block size (build knobs for A/B
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
     const uint64_t w = words[i];
     const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
     keys[i] = td_skey::to_key(w & ((1ull << OTH_TD_SKEY_BITS) - 1));
-    values[i] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
+    values[i] = (double)vs * lam_pow[td_turn_idx(w)];
 }
 
 // ---------------------------------------------------------------------------
@@ -90,11 +97,13 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
 #ifndef OTH_SORT_DIGIT
 #define OTH_SORT_DIGIT 9
 #endif
+// tiles of 8 waves x 32 rounds = 16,384 words (round 5 A/B over 4,096-16,384:
+// fewer, larger tiles shorten the look-back chains; profiles/r05_notes.md)
 #ifndef OTH_SORT_WAVES
-#define OTH_SORT_WAVES 4
+#define OTH_SORT_WAVES 8
 #endif
 #ifndef OTH_SORT_ROUNDS
-#define OTH_SORT_ROUNDS 16
+#define OTH_SORT_ROUNDS 32
 #endif
 #ifndef OTH_SORT_GROUP
 #define OTH_SORT_GROUP 16
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
         if (UNPACK) {
             const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
             keys_out[pos] = td_skey::to_key(w & ((1ull << OTH_TD_SKEY_BITS) - 1));
-            vals_out[pos] = (double)vs * lam_pow[(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK];
+            vals_out[pos] = (double)vs * lam_pow[td_turn_idx(w)];
         } else {
             out[pos] = w;
         }
@@ -1062,7 +1071,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         const int64_t i = base + r * 64 + lane;
         if (WORDS && WRITE && i < n) {
             const int vs = (int)(payload[r] >> (OTH_TD_PACK_VALUE_SHIFT - OTH_TD_PACK_TURN_SHIFT)) - 64;
-            values[i] = (double)vs * lam_pow[payload[r] & OTH_TD_PACK_TURN_MASK];
+            values[i] = (double)vs * lam_pow[min(payload[r] & OTH_TD_PACK_TURN_MASK, (uint32_t)OTH_POS_STRIDE - 1u)];
         }
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;

@@ -225,3 +225,14 @@ def test_td_sort_unpack_and_segments_words_host_build():
     want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
     assert int(cnt[1]) == len(want)
     np.testing.assert_array_equal(li[:len(want)], want)
+
+
+def test_td_unpack_clamps_turn_left_host_build():
+    """A packed word whose turn_left field exceeds 128 (not one
+    oth_td_updates_packed writes) reads lam_pow[128], never past the table."""
+    lam = np.array([0.9 ** j for j in range(129)], np.float64)
+    tl = np.array([0, 128, 129, 0xFFFFF], np.uint64)
+    w = np.ascontiguousarray((np.uint64(64 + 3) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)))
+    keys, vals = np.zeros(4, np.int64), np.zeros(4, np.float64)
+    assert lib().oth_td_unpack(P(w), P(lam), P(keys), P(vals), 4, None) == 0
+    np.testing.assert_array_equal(vals, 3.0 * lam[[0, 128, 128, 128]])

@@ -462,6 +462,25 @@ def test_td_segments_pair():
         np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
 
 
+def test_td_unpack_clamps_turn_left_pair():
+    """Words whose turn_left exceeds 128 (not from oth_td_updates_packed):
+    both builds read lam_pow[128], in oth_td_unpack and in
+    oth_td_segments_words, never past the table."""
+    lam = Buf(np.array([0.9 ** j for j in range(129)], np.float64))
+    tl = np.array([0, 128, 129, 0xFFFFF] * 16, np.uint64)
+    w = Buf((np.uint64(64 - 5) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)))
+    n = len(tl)
+    keys, vals = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64))
+    both("oth_td_unpack", w, lam, keys, vals, n)
+    same(keys, vals)
+    np.testing.assert_array_equal(vals.h, -5.0 * lam.h[np.minimum(tl, 128).astype(np.int64)])
+    off, uk, li, cnt, val = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.int64)),
+                             Buf(np.zeros(2, np.int64)), Buf(np.zeros(n, np.float64)))
+    both_scratch("oth_td_segments_words", w, lam, n, 48, off, uk, li, cnt, val)
+    same(cnt, val)
+    np.testing.assert_array_equal(val.h, vals.h)
+
+
 def test_td_segments_words_pair():
     """oth_td_segments_words (round 5): the same runs read from skey-sorted
     packed words (payloads in the top 28 bits, which must not split a run),

@@ -1019,8 +1019,10 @@ constexpr int kSegWaveKeys = 64 * kSegRounds;
 constexpr int kSegBlock = 256;
 constexpr int kSegWavesPerBlock = kSegBlock / 64;
 // A segment that starts at i is long iff keys[i + long_min - 1] is its key
-// (the keys are sorted), read from the wave's keys staged in LDS (with the
-// next round's).  Both passes find starts and long starts; the count pass
+// (the keys are sorted), taken from the lane long_min - 1 places on in the
+// wave's registers (this round's keys or the next round's, by __shfl; round
+// 5: staged in LDS before, whose 35 KiB per block held the count pass to 4
+// blocks per CU), or from memory for long_min > 65.  Both passes find starts and long starts; the count pass
 // leaves the wave's two counts, the write pass (after their scans) places
 // both in order.  (The long keys by atomic appends instead: 25k appends to
 // one counter cost the write pass 83 -> 368 us.)
@@ -1038,32 +1040,26 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
                                                            int64_t* __restrict__ long_idx,
                                                            const double* __restrict__ lam_pow = nullptr,
                                                            double* __restrict__ values = nullptr) {
-    __shared__ int64_t stage[kSegWavesPerBlock][kSegWaveKeys + 64];
     constexpr int64_t kKeyMask = (1ll << OTH_TD_SKEY_BITS) - 1;
     auto key_of = [](int64_t x) { return WORDS ? (x & kKeyMask) : x; };
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
     const int64_t base = w * kSegWaveKeys;
     if (base >= n) return;  // wave-uniform
-    // every round's key loaded before the first is used (17 loads in flight)
-    int64_t k[kSegRounds];
-    uint32_t payload[kSegRounds];  // WORDS, WRITE: the word's top 21 bits
+    // every round's key loaded before the first is used (17 loads in flight:
+    // k[kSegRounds] is the next wave's first round)
+    int64_t k[kSegRounds + 1];
+    uint32_t payload[kSegRounds];  // WORDS, WRITE: the word's top 28 bits
 #pragma unroll
-    for (int r = 0; r < kSegRounds; r++) {
+    for (int r = 0; r <= kSegRounds; r++) {
         const int64_t i = base + r * 64 + lane;
         const int64_t x = i < n ? keys[i] : 0;
         k[r] = key_of(x);
-        payload[r] = (uint32_t)((uint64_t)x >> OTH_TD_PACK_TURN_SHIFT);
+        if (r < kSegRounds) payload[r] = (uint32_t)((uint64_t)x >> OTH_TD_PACK_TURN_SHIFT);
     }
-    int64_t* mine = stage[threadIdx.x >> 6];
-    {
-        const int64_t i = base + kSegWaveKeys + lane;
-        mine[kSegWaveKeys + lane] = i < n ? key_of(keys[i]) : -1;  // (keys are >= 0)
-    }
-#pragma unroll
-    for (int r = 0; r < kSegRounds; r++) mine[r * 64 + lane] = k[r];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    const int ahead = (int)long_min - 1;  // (wave-uniform)
+    const bool by_shfl = ahead <= 64;
+    const int src = (lane + ahead) & 63;
     int64_t prev_last = base > 0 ? key_of(keys[base - 1]) : 0;
     int64_t pos = WRITE ? wave_cnt[w] : 0, lpos = WRITE ? wave_lcnt[w] : 0;  // after the scans: the wave's firsts
 #pragma unroll
@@ -1076,8 +1072,14 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
         const bool start = i < n && (i == 0 || k[r] != before);
-        const int64_t e = i + long_min - 1, off = e - base;
-        const bool lng = start && e < n && (off < kSegWaveKeys + 64 ? mine[off] == k[r] : key_of(keys[e]) == k[r]);
+        const int64_t e = i + long_min - 1;
+        bool lng = false;
+        if (by_shfl) {
+            const int64_t here = __shfl(k[r], src), next = __shfl(k[r + 1], src);
+            lng = start && e < n && (lane + ahead < 64 ? here : next) == k[r];
+        } else {
+            lng = start && e < n && key_of(keys[e]) == k[r];
+        }
         const uint64_t m = __ballot(start), ml = __ballot(lng);
         if (WRITE && start) {
             const int64_t at =

@@ -434,20 +434,23 @@ def test_td_pair():
     np.testing.assert_array_equal(out2.h, out.h)
 
 
-def test_td_segments_pair():
+@pytest.mark.parametrize("long_min", [48, 1, 2, 64, 65, 66, 1000])
+def test_td_segments_pair(long_min):
     """oth_td_segments: the runs of a key-sorted stream (short, long, a
     single-key stream's one run, runs crossing the GPU's 64-key rounds and
     1,024-key waves) -- offsets and keys equal on both builds and to numpy's,
-    the long segments the same set."""
+    the long segments the same set.  long_min up to 65 takes the GPU's
+    register path (the key long_min - 1 places on by __shfl, round 5), beyond
+    it the load from memory."""
     rng = np.random.default_rng(12)
-    for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 1023, 1024, 1025, 5000],
-                                                                          400)):
+    for lens in (rng.integers(1, 5, 3000), np.array([70000]), rng.choice([1, 2, 47, 48, 49, 63, 64, 65, 66, 1023, 1024,
+                                                                           1025, 5000], 400)):
         keys = np.repeat(np.cumsum(rng.integers(1, 1000, len(lens))).astype(np.int64), lens)
         n = len(keys)
         k = Buf(keys)
         off, uk, li, cnt = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.int64)),
                             Buf(np.zeros(2, np.int64)))
-        both_scratch("oth_td_segments", k, n, 48, off, uk, li, cnt)
+        both_scratch("oth_td_segments", k, n, long_min, off, uk, li, cnt)
         same(cnt)
         m, nl = (int(x) for x in cnt.h)
         starts = np.flatnonzero(np.r_[True, keys[1:] != keys[:-1]])
@@ -456,7 +459,7 @@ def test_td_segments_pair():
         np.testing.assert_array_equal(uk.h[:m], keys[starts])
         np.testing.assert_array_equal(off.d.cpu().numpy()[:m + 1], off.h[:m + 1])
         np.testing.assert_array_equal(uk.d.cpu().numpy()[:m], uk.h[:m])
-        want = np.flatnonzero(np.diff(np.r_[starts, n]) >= 48)
+        want = np.flatnonzero(np.diff(np.r_[starts, n]) >= long_min)
         assert nl == len(want)
         np.testing.assert_array_equal(li.h[:nl], want)
         np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)

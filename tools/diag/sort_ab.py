@@ -61,6 +61,8 @@ for tag, L in zip(["rocprim"] + [os.path.basename(p)[:-3] for p in paths[1:]], l
     v = torch.empty(n, dtype=torch.float64, device=dev)
     a = (words.data_ptr(), o.data_ptr(), n, t.data_ptr(), ctypes.byref(tb), s)
     variants.append((tag + " sort_packed", L.oth_td_sort_packed, a, o, None))
+    if "nolook" in tag:  # diagnostic builds whose output is unsorted by design: the sort alone
+        continue
     ua = (o.data_ptr(), lam.data_ptr(), k.data_ptr(), v.data_ptr(), n, s)
     variants.append((tag + " unpack", L.oth_td_unpack, ua, None, None))
     if tag != "rocprim":

@@ -1778,7 +1778,10 @@ constexpr int64_t kSpecMaxLen = 1ll << 27;  // longer keys (beyond any batch in 
 // keys of >= 3 warm-ups are split (at a = 0.03: 5,826 updates, the single-lane
 // chain's longest as in round 3; at 4 warm-ups of the longer round-4 warm-up,
 // 7,768, the long-key kernel took 199 us against 130)
-constexpr int64_t kSpecMinWarms = 3;
+#ifndef OTH_SPEC_MIN_WARMS  // A/B builds
+#define OTH_SPEC_MIN_WARMS 3
+#endif
+constexpr int64_t kSpecMinWarms = OTH_SPEC_MIN_WARMS;
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
@@ -2002,7 +2005,12 @@ inline size_t spec_scratch_bytes(int64_t n_long, int64_t n_values) {
 // 262,144-game batch took ~13 ms); here the whole wave stages the segment
 // through LDS with coalesced loads, double-buffered, and lane 0 runs the chain
 // from LDS while the next stage is in flight, so the time is the chain's.
-constexpr int kTdStage = 1024;                 // doubles per LDS stage
+// (round 5: 1,024 before; at 33 KiB of LDS per one-wave block only 4 keys'
+// chains ran per CU: 131 -> 92 us per batch at 512, 106-110 at 256)
+#ifndef OTH_TD_STAGE  // A/B builds
+#define OTH_TD_STAGE 512
+#endif
+constexpr int kTdStage = OTH_TD_STAGE;         // doubles per LDS stage
 constexpr int kTdStageLoads = kTdStage / 64;   // loads per lane per stage
 __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ vals,
                                                          const int64_t* __restrict__ seg_off,

@@ -70,7 +70,7 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
     redoes the chunk otherwise: plant exact zero states (a = 0.5, x = -v) at
     chunk starts, middles and ends of long segments and compare with the
     sequential rule in Python floats.  With long_min, oth_td_ema_split runs
-    the segments at least that long on a whole wave each (LDS stages of 1024
+    the segments at least that long on a whole wave each (LDS stages of 512
     values: lengths around multiples of the stage), those at least 3 warm-ups
     long split into parts over many waves (warm-up 86 at a = 0.5).  A
     warm-up of 1 or 3 values (OTH_TD_SPEC_WARM) makes most guesses miss: the
@@ -80,7 +80,7 @@ def test_td_ema_zero_states_in_long_segments(long_min, spec_warm, monkeypatch):
         monkeypatch.setenv("OTH_TD_SPEC_WARM", spec_warm)
     a, oma = 0.5, 0.5
     rng = np.random.default_rng(11)
-    lengths = [1, 5, 47, 48, 49, 63, 64, 100, 1000, 1023, 1024, 1025, 2048, 4099, 12345]
+    lengths = [1, 5, 47, 48, 49, 63, 64, 100, 511, 512, 513, 1000, 1023, 1024, 1025, 2048, 4099, 12345]
     vals, seg, want = [], [0], []
     for L in lengths:
         v = 0.0 if L % 2 else 0.25

@@ -15,7 +15,7 @@ for x in rows:
     if 'rollout' in nm:
         continue
     tot += float(x['TotalDurationNs'])
-    if any(k in nm for k in ('td_merge', 'td_lookup', 'td_splits', 'td_seg_kernel', 'td_updates', 'td_ema')):
+    if any(k in nm for k in ('td_merge', 'td_lookup', 'td_splits', 'td_seg_kernel', 'td_updates', 'td_ema', 'replay')):
         print("%-12s %-44s avg %8.1f us calls %s" % (sys.argv[2], nm[:44], float(x['AverageNs']) / 1e3, x['Calls']))
 print("%-12s kernels other than the rollout: %.3f ms per batch (4 batches)" % (sys.argv[2], tot / 4e6))
 PY

@@ -616,7 +616,12 @@ template <int POLICY, bool RECORD, bool RUNNER = false>
 #ifndef OTH_EVAL_WAVES_PER_SIMD  // A/B builds: the eval kernels' occupancy floor (launch bounds)
 #define OTH_EVAL_WAVES_PER_SIMD 4
 #endif
-__global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL ? OTH_EVAL_WAVES_PER_SIMD : 4) void rollout_kernel(
+#ifndef OTH_GREEDY_WAVES_PER_SIMD  // A/B builds: the greedy kernels' occupancy floor
+#define OTH_GREEDY_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WAVES_PER_SIMD
+                                     : POLICY == OTH_POLICY_GREEDY ? OTH_GREEDY_WAVES_PER_SIMD
+                                                                   : 4) void rollout_kernel(
     RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
     const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();

@@ -195,6 +195,13 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 #ifndef OTH_COOP_HOLD_EVAL  // round 5: the eval kernel holds its parent record too (A/B: 0 rereads it)
 #define OTH_COOP_HOLD_EVAL 1
 #endif
+// OTH_COOP_FORCED=1 (A/B builds only): a mover with exactly one legal move plays
+// it without scoring its child (same games: no RNG is drawn either way).  It
+// cut greedy VALU by 0.9% but ran 1.3% (greedy) / 5% (eval) slower per launch
+// (round 5, tools/diag/forced_ab.sh, profiles/r05_notes.md)
+#ifndef OTH_COOP_FORCED
+#define OTH_COOP_FORCED 0
+#endif
 struct CoopWave {
     u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words; A1's bit 0, a1, carries the eval table)
     u64 legal[64];    // parent lane's legal mask (0: not choosing)
@@ -883,11 +890,14 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
                                 sq = pick_legal(legal, rng, kth_tab);
                                 if (side == OTH_BLACK) rem_b--;
                                 else rem_w--;
+                            } else if (OTH_COOP_FORCED && !(legal & (legal - 1))) {
+                                sq = (u32)__builtin_ctzll(legal);  // one legal move: no children to score
                             } else {
                                 choose = true;
                             }
                         } else if ((int)ply >= a.n_random) {
-                            choose = true;  // decided below, by the whole wave
+                            if (OTH_COOP_FORCED && !(legal & (legal - 1))) sq = (u32)__builtin_ctzll(legal);
+                            else choose = true;  // decided below, by the whole wave
                         } else {
                             sq = pick_legal(legal, rng, kth_tab);
                         }

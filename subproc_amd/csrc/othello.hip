@@ -1579,11 +1579,39 @@ __global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restric
 // leaves about half the lanes of the waves that do work idle (a game records
 // ~62 positions of its 129 slots, and the waves straddle games); here a wave
 // idles only on the lanes past the game's own positions.  The game's plies,
-// row offset, base and terminal row are wave-uniform (scalar loads).
+// row offset, base and terminal row are wave-uniform (scalar loads).  A wave
+// takes OTH_TD_UPD_GAMES = 4 games (late round 5): 195 -> 177 us per 32.2M
+// updates (1: 195, 2: 179-183, 8: 175-177 at 112 VGPRs; tools/diag/td_ab.sh).
 // OTH_TD_UPD_WAVE=0 builds the per-slot kernel for these entry points (A/B).
 #ifndef OTH_TD_UPD_WAVE
 #define OTH_TD_UPD_WAVE 1
 #endif
+// OTH_TD_UPD_GAMES games per wave, one after the other: their scalar loads
+// (plies, row offset, base, terminal row) and first-round row loads are issued
+// before any game's words are computed, so a wave waits on one dependent
+// chain of loads for all of them instead of one chain per game.
+#ifndef OTH_TD_UPD_GAMES
+#define OTH_TD_UPD_GAMES 4
+#endif
+// the words (or key/value pairs) of position p of a game whose terminal
+// position np gives value_for_black vb; first update index jb
+template <bool WORDS>
+__device__ __forceinline__ void td_update_pair(ulonglong2 b, u32 p, u32 np, int vb, int64_t jb,
+                                               const double* __restrict__ lam_pow, int64_t* __restrict__ keys,
+                                               double* __restrict__ vals, u64* __restrict__ words) {
+    const int64_t j = jb + 2 * (int64_t)(np - p);
+    if (WORDS) {
+        const u64 t = (u64)(np - p) << OTH_TD_PACK_TURN_SHIFT;
+        words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
+        words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
+        return;
+    }
+    const double lam = lam_pow[np - p];
+    keys[j] = td_key(b, OTH_BLACK);
+    vals[j] = (double)vb * lam;
+    keys[j + 1] = td_key(b, OTH_WHITE);
+    vals[j + 1] = (double)(-vb) * lam;
+}
 template <bool WORDS>
 __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __restrict__ pos,
                                                                  const int64_t* __restrict__ row_off,
@@ -1592,28 +1620,34 @@ __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __re
                                                                  const double* __restrict__ lam_pow,
                                                                  int64_t* __restrict__ keys, double* __restrict__ vals,
                                                                  u64* __restrict__ words, int64_t n) {
-    const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (g >= n) return;
+    constexpr int G = OTH_TD_UPD_GAMES;
+    const int64_t g0 =
+        ((int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) * G;
+    if (g0 >= n) return;
     const u32 lane = threadIdx.x & 63u;
-    const u32 np = min<u32>(plies[g], OTH_MOVES_STRIDE);
-    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + (row_off ? row_off[g] : g * OTH_POS_STRIDE);
-    const ulonglong2 term = row[np];
-    const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
-    const int64_t jb = base[g];
-    for (u32 p = lane; p <= np; p += 64) {
-        const ulonglong2 b = row[p];
-        const int64_t j = jb + 2 * (int64_t)(np - p);
-        if (WORDS) {
-            const u64 t = (u64)(np - p) << OTH_TD_PACK_TURN_SHIFT;
-            words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
-            words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
-            continue;
-        }
-        const double lam = lam_pow[np - p];
-        keys[j] = td_key(b, OTH_BLACK);
-        vals[j] = (double)vb * lam;
-        keys[j + 1] = td_key(b, OTH_WHITE);
-        vals[j + 1] = (double)(-vb) * lam;
+    const int ng = (int)min<int64_t>(G, n - g0);  // wave-uniform
+    u32 np[G];
+    const ulonglong2* row[G];
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+        const int64_t g = g0 + min(k, ng - 1);  // a game past n repeats the last one; never written
+        np[k] = min<u32>(plies[g], OTH_MOVES_STRIDE);
+        row[k] = reinterpret_cast<const ulonglong2*>(pos) + (row_off ? row_off[g] : g * OTH_POS_STRIDE);
+    }
+    ulonglong2 term[G], b[G];
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+        term[k] = row[k][np[k]];
+        b[k] = row[k][min(lane, np[k])];  // lanes past the game's positions reread its terminal row
+    }
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+        if (k >= ng) break;
+        const int vb = __popcll(term[k].x) - __popcll(term[k].y);  // value_for_black (41); white gets -vb (42)
+        const int64_t jb = base[g0 + k];
+        if (lane <= np[k]) td_update_pair<WORDS>(b[k], lane, np[k], vb, jb, lam_pow, keys, vals, words);
+        for (u32 p = lane + 64; p <= np[k]; p += 64)  // games of more than 63 plies
+            td_update_pair<WORDS>(row[k][p], p, np[k], vb, jb, lam_pow, keys, vals, words);
     }
 }
 
@@ -2197,7 +2231,8 @@ inline int launched() { return status(hipGetLastError()); }
 static int td_updates_launch(const u64* pos, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                              const double* lam_pow, int64_t* keys, double* vals, u64* words, int64_t n, hipStream_t s) {
     if (OTH_TD_UPD_WAVE)
-        (words ? td_updates_wave_kernel<true> : td_updates_wave_kernel<false>)<<<blocks_for(n * 64), kBlock, 0, s>>>(
+        (words ? td_updates_wave_kernel<true> : td_updates_wave_kernel<false>)<<<
+            blocks_for((n + OTH_TD_UPD_GAMES - 1) / OTH_TD_UPD_GAMES * 64), kBlock, 0, s>>>(
             pos, row_off, plies, base, lam_pow, keys, vals, words, n);
     else
         td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys,

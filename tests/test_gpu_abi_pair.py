@@ -434,6 +434,40 @@ def test_td_pair():
     np.testing.assert_array_equal(out2.h, out.h)
 
 
+def test_td_updates_ragged_long_pair():
+    """The update stream for a game count that is no multiple of the kernel's
+    games per wave (OTH_TD_UPD_GAMES) and for games of 0 to 128 plies (positions
+    64 and on take the lanes' second round): synthetic disjoint boards, every
+    layout and output form, both builds bit for bit."""
+    rng = np.random.default_rng(11)
+    pl = np.array([0, 1, 5, 63, 64, 65, 127, 128, 60, 2, 100], np.uint8)
+    n = len(pl)
+    b = rng.integers(0, 2 ** 63, (n, _lib.POS_STRIDE), dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, (n, _lib.POS_STRIDE), dtype=np.uint64)
+    w = rng.integers(0, 2 ** 63, (n, _lib.POS_STRIDE), dtype=np.uint64) & ~b
+    pos = Buf(np.stack([b, w], axis=-1))
+    rows = pl.astype(np.int64) + 1
+    off = Buf(np.cumsum(rows) - rows)
+    prow = Buf(np.concatenate([pos.h[g, :rows[g]] for g in range(n)]))
+    plies = Buf(pl)
+    cnt = 2 * rows
+    base = Buf(np.cumsum(cnt) - cnt)
+    total = int(cnt.sum())
+    lam = Buf(np.array([0.9 ** k for k in range(_lib.POS_STRIDE)], np.float64))
+    keys, vals = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+    both("oth_td_updates", pos, plies, base, lam, keys, vals, n)
+    same(keys, vals)
+    keys2, vals2 = Buf(np.zeros(total, np.int64)), Buf(np.zeros(total, np.float64))
+    both("oth_td_updates_rows", prow, off, plies, base, lam, keys2, vals2, n)
+    same(keys2, vals2)
+    np.testing.assert_array_equal(keys2.h, keys.h)
+    for po, layout in ((None, pos), (off, prow)):
+        words = Buf(np.zeros(total, np.uint64))
+        both("oth_td_updates_packed", layout, po, plies, base, words, n)
+        same(words)
+        np.testing.assert_array_equal(skeys_to_keys((words.h & np.uint64((1 << _lib.TD_SKEY_BITS) - 1)).astype(np.int64)),
+                                      keys.h)
+
+
 @pytest.mark.parametrize("long_min", [48, 1, 2, 64, 65, 66, 1000])
 def test_td_segments_pair(long_min):
     """oth_td_segments: the runs of a key-sorted stream (short, long, a

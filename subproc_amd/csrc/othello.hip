@@ -2501,6 +2501,71 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
     return launched();
 }
 
+// Fork / join of the TD EMA's side streams (round 5).  The long keys' waves
+// and the split keys' chain are latency-bound (a few thousand dependent
+// chains) and ran after the short keys' kernel on the caller's stream; on two
+// non-blocking side streams of the device they run beside it.  The side
+// streams wait on an event recorded on the caller's stream at the fork, and
+// the caller's stream waits on one event per side stream at the join, so
+// everything after the call (on the caller's stream) sees all three kernels'
+// outputs, as a single-stream call would.  A per-device mutex holds the fork
+// to the join (the events are the device's, shared by every caller).
+// OTH_TD_EMA_FORK=0 in the environment keeps every launch on the caller's
+// stream (A/B).
+struct TdSides {
+    std::mutex mu;
+    bool made = false;
+    int rc = OTH_OK;
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
+TdSides g_td_sides[kMaxDevices];
+struct TdFork {
+    TdSides* d = nullptr;
+    hipStream_t s;
+    int n = 0, rc = OTH_OK;
+    std::unique_lock<std::mutex> lock;
+    TdFork(hipStream_t caller, int n_sides) : s(caller) {
+        static const int enabled = env_int("OTH_TD_EMA_FORK", 1);
+        int dev = 0;
+        if (n_sides <= 0 || !enabled || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
+        d = &g_td_sides[dev];
+        lock = std::unique_lock<std::mutex>(d->mu);
+        if (!d->made) {
+            d->made = true;
+            // the side streams at the device's highest priority: their chains
+            // are the EMA's critical path, so their waves take CU slots first
+            int least = 0, greatest = 0;
+            hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+            if (!env_int("OTH_TD_EMA_PRIO", 1)) greatest = least;
+            for (int k = 0; k < 2 && e == hipSuccess; k++) {
+                e = hipStreamCreateWithPriority(&d->side[k], hipStreamNonBlocking, greatest);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&d->join[k], hipEventDisableTiming);
+            }
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&d->fork, hipEventDisableTiming);
+            d->rc = status(e);
+        }
+        if ((rc = d->rc) != OTH_OK) return;
+        rc = status(hipEventRecord(d->fork, s));
+        for (int k = 0; k < n_sides && rc == OTH_OK; k++) {
+            rc = status(hipStreamWaitEvent(d->side[k], d->fork, 0));
+            if (rc == OTH_OK) n = k + 1;
+        }
+    }
+    hipStream_t side(int k) const { return n > k ? d->side[k] : s; }
+    // the caller's stream waits for the side streams; the first error wins
+    int join(int rc0) {
+        for (int k = 0; k < n; k++) {
+            const int r = status(hipEventRecord(d->join[k], d->side[k]));
+            const int w = r == OTH_OK ? status(hipStreamWaitEvent(s, d->join[k], 0)) : r;
+            if (rc0 == OTH_OK) rc0 = w;
+        }
+        n = 0;
+        return rc0;
+    }
+    ~TdFork() { join(OTH_OK); }
+};
+
 // warm-up length of the split's guesses for the rule's contraction |1 - a|:
 // 4/3 of the smallest w with |1 - a|^w < 2^-64 (at w itself the two runs are
 // still one ulp apart now and then: 4 misses among the first 40 split keys of
@@ -2518,6 +2583,36 @@ static int64_t td_spec_warm(double oma) {
     return w > (double)(1 << 20) ? 0 : (int64_t)w;
 }
 
+// the split keys: plan, parts (one wave per 64 parts), check and reruns, on stream s
+static int td_spec_launch(const double* values, const int64_t* seg_off, const double* init, double a,
+                          double one_minus_a, double* out, const int64_t* long_idx, int64_t n_long, int64_t n_values,
+                          int64_t warm, void* temp, hipStream_t s) {
+    int64_t* hdr = static_cast<int64_t*>(temp);
+    SpecPlanEntry* plan = reinterpret_cast<SpecPlanEntry*>(hdr + kSpecHdr);
+    double* guess = reinterpret_cast<double*>(plan + std::max<int64_t>(n_long, 1));
+    const int64_t parts = n_values / kSpecLen + n_long + 1;
+    double* fin = guess + parts;
+    const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
+    const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, s);
+    if (me != hipSuccess) return status(me);
+    td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, s>>>(seg_off, long_idx, n_long, kSpecMinWarms * warm, hdr,
+                                                                 plan);
+    int rc = launched();
+    if (rc != OTH_OK) return rc;
+    td_spec_plan_kernel<<<1, 1024, 0, s>>>(hdr, plan, parts);
+    rc = launched();
+    if (rc != OTH_OK) return rc;
+    const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
+    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, s>>>(values, seg_off, init, a, one_minus_a, hdr, plan, guess,
+                                                                 fin, warm16);
+    rc = launched();
+    if (rc != OTH_OK) return rc;
+    td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, s>>>(values, seg_off, init, a,
+                                                                                         one_minus_a, hdr, plan, guess,
+                                                                                         fin, out);
+    return launched();
+}
+
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
                      int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream) {
@@ -2532,43 +2627,29 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     }
     if (*temp_bytes < need) return OTH_EINVAL;
     if (n_seg == 0) return OTH_OK;
+    // the long keys (one wave each) and the split keys (plan, parts, check and
+    // reruns) on the device's two side streams, launched first, beside the
+    // short keys' kernel on the caller's stream: the three write disjoint
+    // outputs and read only what the caller's stream did before this call
+    const hipStream_t s = (hipStream_t)stream;
+    TdFork fork(s, n_long == 0 ? 0 : (warm > 0 ? 2 : 1));
+    if (fork.rc != OTH_OK) return fork.rc;
+    int rc = OTH_OK;
+    if (n_long > 0) {
+        td_ema_long_kernel<<<(unsigned)n_long, 64, 0, fork.side(0)>>>(values, seg_off, init, a, one_minus_a, out,
+                                                                       long_idx, warm);
+        rc = launched();
+    }
+    if (rc == OTH_OK && n_long > 0 && warm > 0) rc = td_spec_launch(values, seg_off, init, a, one_minus_a, out, long_idx,
+                                                                    n_long, n_values, warm, temp, fork.side(1));
+    if (rc != OTH_OK) return fork.join(rc);
     if (long_min <= 3 * kTdChunk)
-        td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
-                                                                                   one_minus_a, out, n_seg, long_min);
+        td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, s>>>(values, seg_off, init, a, one_minus_a, out, n_seg,
+                                                                 long_min);
     else
-        td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
-                                                                                    one_minus_a, out, n_seg, long_min);
-    int rc = launched();
-    if (rc != OTH_OK || n_long == 0) return rc;
-    td_ema_long_kernel<<<(unsigned)n_long, 64, 0, (hipStream_t)stream>>>(values, seg_off, init, a, one_minus_a,
-                                                                         out, long_idx, warm);
-    rc = launched();
-    if (rc != OTH_OK || warm <= 0) return rc;
-    // the split keys: plan, parts (one wave per 64 parts), check and reruns
-    int64_t* hdr = static_cast<int64_t*>(temp);
-    SpecPlanEntry* plan = reinterpret_cast<SpecPlanEntry*>(hdr + kSpecHdr);
-    double* guess = reinterpret_cast<double*>(plan + std::max<int64_t>(n_long, 1));
-    const int64_t parts = n_values / kSpecLen + n_long + 1;
-    double* fin = guess + parts;
-    const int warm16 = (int)((warm + kTdChunk - 1) / kTdChunk * kTdChunk);
-    const hipError_t me = hipMemsetAsync(hdr, 0, sizeof(int64_t) * kSpecHdr, (hipStream_t)stream);
-    if (me != hipSuccess) return status(me);
-    td_spec_select_kernel<<<blocks_for(n_long), kBlock, 0, (hipStream_t)stream>>>(seg_off, long_idx, n_long,
-                                                                                    kSpecMinWarms * warm, hdr, plan);
-    rc = launched();
-    if (rc != OTH_OK) return rc;
-    td_spec_plan_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(hdr, plan, parts);
-    rc = launched();
-    if (rc != OTH_OK) return rc;
-    const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
-    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, (hipStream_t)stream>>>(values, seg_off, init, a,
-                                                                                   one_minus_a, hdr, plan, guess,
-                                                                                   fin, warm16);
-    rc = launched();
-    if (rc != OTH_OK) return rc;
-    td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, (hipStream_t)stream>>>(
-        values, seg_off, init, a, one_minus_a, hdr, plan, guess, fin, out);
-    return launched();
+        td_ema_kernel<false><<<blocks_for(n_seg), kBlock, 0, s>>>(values, seg_off, init, a, one_minus_a, out, n_seg,
+                                                                  long_min);
+    return fork.join(launched());
 }
 
 int oth_rollout_grid(int policy, int64_t n) {

@@ -1751,6 +1751,9 @@ __device__ __forceinline__ double td_range(double v, const double* __restrict__ 
 // SHORT: every segment here is shorter than 3 chunks (long_min <= 3 * kTdChunk),
 // so the kernel has no ring of loads and needs a fraction of the registers:
 // more waves in flight for the millions of 1- to 3-update keys.
+#ifndef OTH_TD_EMA_PRE  // A/B builds
+#define OTH_TD_EMA_PRE 8
+#endif
 template <bool SHORT>
 __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
                                                         const int64_t* __restrict__ seg_off,
@@ -1763,7 +1766,17 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
     if (long_min > 0 && e - i >= long_min) return;
     double v = init ? init[s] : 0.0;
     if (SHORT) {
-        for (; i < e; i++) v = td_step(v, vals[i], a, oma);
+        // the first OTH_TD_EMA_PRE values loaded together (predicated), so
+        // most keys (1 to a few updates) wait on one round trip for them
+        // rather than one per update; the rest one by one
+        constexpr int kPre = OTH_TD_EMA_PRE;
+        double x[kPre > 0 ? kPre : 1];
+#pragma unroll
+        for (int k = 0; k < kPre; k++) x[k] = i + k < e ? vals[i + k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < kPre; k++)
+            if (i + k < e) v = td_step(v, x[k], a, oma);
+        for (i += kPre; i < e; i++) v = td_step(v, vals[i], a, oma);
         out[s] = v;
     } else {
         out[s] = td_range(v, vals, i, e, a, oma);
@@ -1914,9 +1927,15 @@ __global__ __launch_bounds__(kBlock) void td_spec_select_kernel(const int64_t* _
 // would end past cap (n_values below seg_off[n_seg], a caller error the
 // header names) gets no parts and no work items: td_spec_fix_kernel then runs
 // it sequentially, so no part is ever written out of bounds.
-__global__ __launch_bounds__(1024) void td_spec_plan_kernel(int64_t* __restrict__ hdr,
-                                                            SpecPlanEntry* __restrict__ plan, int64_t cap) {
-    __shared__ u32 wsum[2][16];
+// one block of kPlanThreads: beside the short keys' kernel (the EMA's side
+// streams) a block of 1,024 threads waited 40-67 us for a CU with room for it
+#ifndef OTH_TD_PLAN_THREADS  // A/B builds
+#define OTH_TD_PLAN_THREADS 256
+#endif
+constexpr int kPlanThreads = OTH_TD_PLAN_THREADS, kPlanWaves = kPlanThreads / 64;
+__global__ __launch_bounds__(kPlanThreads) void td_spec_plan_kernel(int64_t* __restrict__ hdr,
+                                                                    SpecPlanEntry* __restrict__ plan, int64_t cap) {
+    __shared__ u32 wsum[2][kPlanWaves];
     __shared__ int64_t carry[2];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t n_spec = hdr[3];
@@ -1932,7 +1951,7 @@ __global__ __launch_bounds__(1024) void td_spec_plan_kernel(int64_t* __restrict_
         for (int w2 = 0; w2 < wv; w2++) before += wsum[c][w2];
         return carry[c] + before + incl - x;
     };
-    for (int64_t t0 = 0; t0 < n_spec; t0 += 1024) {
+    for (int64_t t0 = 0; t0 < n_spec; t0 += kPlanThreads) {
         const int64_t k = t0 + t;
         u32 P = k < n_spec ? (u32)plan[k].n_parts : 0u;
         const int64_t pbase = block_excl(P, 0);
@@ -1947,7 +1966,7 @@ __global__ __launch_bounds__(1024) void td_spec_plan_kernel(int64_t* __restrict_
         __syncthreads();
         if (t < 2) {
             u32 tot = 0;
-            for (int w2 = 0; w2 < 16; w2++) tot += wsum[t][w2];
+            for (int w2 = 0; w2 < kPlanWaves; w2++) tot += wsum[t][w2];
             carry[t] += tot;
         }
         __syncthreads();
@@ -2599,7 +2618,7 @@ static int td_spec_launch(const double* values, const int64_t* seg_off, const do
                                                                  plan);
     int rc = launched();
     if (rc != OTH_OK) return rc;
-    td_spec_plan_kernel<<<1, 1024, 0, s>>>(hdr, plan, parts);
+    td_spec_plan_kernel<<<1, kPlanThreads, 0, s>>>(hdr, plan, parts);
     rc = launched();
     if (rc != OTH_OK) return rc;
     const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);

@@ -313,13 +313,13 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
  * parts' guesses and end states), the caller's; temp == NULL is a size query
  * (*temp_bytes receives the size for these n_long and n_values, nothing else
  * happens), otherwise *temp_bytes is the size of temp.  Same results as
- * oth_td_ema, bit for bit.  The long and split segments run on two
- * high-priority side streams of the device (created on first use, kept for
- * the process) beside the short segments' kernel on `stream`: they wait for
- * what `stream` had queued before the call, and `stream` waits for them
- * before anything queued after it, so to the caller the call is ordered on
- * `stream` alone (round 5; OTH_TD_EMA_FORK=0 in the environment keeps every
- * launch on `stream`). */
+ * oth_td_ema, bit for bit.  With OTH_TD_EMA_FORK=1 in the environment
+ * (off by default) the long and split segments run on two high-priority
+ * side streams of the device (created on first use, kept for the process)
+ * beside the short segments' kernel on `stream`: they wait for what
+ * `stream` had queued before the call, and `stream` waits for them before
+ * anything queued after it, so to the caller the call is still ordered on
+ * `stream` alone. */
 int oth_td_ema_split(const double* values, const int64_t* seg_off, const double* init, double a,
                      double one_minus_a, double* out, int64_t n_seg, int64_t long_min, const int64_t* long_idx,
                      int64_t n_long, int64_t n_values, void* temp, size_t* temp_bytes, void* stream);

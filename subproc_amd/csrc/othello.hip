@@ -2529,8 +2529,12 @@ int oth_td_ema(const double* values, const int64_t* seg_off, const double* init,
 // everything after the call (on the caller's stream) sees all three kernels'
 // outputs, as a single-stream call would.  A per-device mutex holds the fork
 // to the join (the events are the device's, shared by every caller).
-// OTH_TD_EMA_FORK=0 in the environment keeps every launch on the caller's
-// stream (A/B).
+// Off by default, on with OTH_TD_EMA_FORK=1 in the environment: alone in a
+// process it took 60-100 us off a 262,144-game batch (2.43 -> 2.33 ms,
+// tools/diag/td_bench_ab.py), but inside bench.py, after the rollout lines
+// have created their own streams, the same batch ran 2.41 -> 2.64 ms with it
+// (the device's few hardware queues are then shared among more streams;
+// profiles/r05_notes.md).
 struct TdSides {
     std::mutex mu;
     bool made = false;
@@ -2545,7 +2549,7 @@ struct TdFork {
     int n = 0, rc = OTH_OK;
     std::unique_lock<std::mutex> lock;
     TdFork(hipStream_t caller, int n_sides) : s(caller) {
-        static const int enabled = env_int("OTH_TD_EMA_FORK", 1);
+        static const int enabled = env_int("OTH_TD_EMA_FORK", 0);
         int dev = 0;
         if (n_sides <= 0 || !enabled || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
         d = &g_td_sides[dev];

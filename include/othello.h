@@ -437,6 +437,17 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
  * allocates nothing. */
 int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                   int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream);
+/* oth_td_lookup with the batch's key count read from device memory when the
+ * call runs on the stream: *n_upd_dev (one int64, device; clamped to
+ * [0, n_upd_max]) is n_upd, e.g. the counts[0] that oth_td_segments(_words)
+ * wrote just before, so the lookup can be queued behind the segments pass
+ * before the host has read that count (round 5: the host's read then
+ * overlaps the lookup).  Scratch (size query from n_old and n_upd_max) and
+ * the arrays are sized for n_upd_max; init / is_new past the count are left
+ * as they were.  Same results as oth_td_lookup with n_upd = *n_upd_dev. */
+int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                      int64_t n_upd_max, const int64_t* n_upd_dev, double* init, uint8_t* is_new, void* temp,
+                      size_t* temp_bytes, void* stream);
 
 /* The batch's results into the table: old_keys (n_old, unique, ascending) with
  * old_vals, and upd_keys (n_upd, unique, ascending) with their new values

@@ -585,6 +585,16 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
     return OTH_OK;
 }
 
+/* the count from (host) memory, clamped as the GPU build clamps it */
+int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                      int64_t n_upd_max, const int64_t* n_upd_dev, double* init, uint8_t* is_new, void* temp,
+                      size_t* temp_bytes, void* stream) {
+    if (n_upd_max < 0 || (temp && n_upd_max > 0 && !n_upd_dev)) return OTH_EINVAL;
+    int64_t n = n_upd_max;
+    if (temp && n_upd_dev) n = *n_upd_dev < 0 ? 0 : (*n_upd_dev > n_upd_max ? n_upd_max : *n_upd_dev);
+    return oth_td_lookup(old_keys, old_vals, n_old, upd_keys, n, init, is_new, temp, temp_bytes, stream);
+}
+
 /* the sorted union, batch values winning (two-pointer merge; new_before is
  * the GPU kernel's placement input and is only bounds-checked here) */
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,

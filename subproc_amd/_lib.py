@@ -63,6 +63,7 @@ SIGNATURES = {
     "oth_td_unpack": (_I, [_P, _P, _P, _P, _I64, _P]),
     "oth_td_merge": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
+    "oth_td_lookup_dev": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "oth_td_fit_moments": (_I, [_P, _P, _I64, _P, _P, _P]),
 }
 

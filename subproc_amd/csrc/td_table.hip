@@ -703,12 +703,19 @@ __device__ __forceinline__ void stage_tile(const int64_t* __restrict__ A, const 
 // ~2,000 per block, which made the HBM traffic of the lookup and the merge
 // 3-4x their algorithmic bytes (profiles/r03_profile_summary.json before
 // this change).  Here all the searches run at once, ~25 loads each.
+// nB_dev (oth_td_lookup_dev): B's length read from device memory, clamped to
+// [0, nB]; the grid is sized for nB
+__device__ __forceinline__ int64_t dev_count(const int64_t* nB_dev, int64_t nB) {
+    return nB_dev ? min(max(*nB_dev, (int64_t)0), nB) : nB;
+}
 __global__ __launch_bounds__(kMergeBlock) void td_splits_kernel(const int64_t* __restrict__ A, int64_t nA,
                                                                 const int64_t* __restrict__ B, int64_t nB,
                                                                 int64_t tile, int64_t nsplit,
-                                                                int64_t* __restrict__ split) {
+                                                                int64_t* __restrict__ split,
+                                                                const int64_t* __restrict__ nB_dev) {
     const int64_t t = (int64_t)blockIdx.x * kMergeBlock + threadIdx.x;
     if (t >= nsplit) return;
+    nB = dev_count(nB_dev, nB);
     const int64_t d = min(t * tile, nA + nB);
     int64_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
     while (lo < hi) {
@@ -886,11 +893,14 @@ __global__ __launch_bounds__(kMergeBlock) void td_lookup_kernel(const int64_t* _
                                                                 const int64_t* __restrict__ B, int64_t nB,
                                                                 const int64_t* __restrict__ split,
                                                                 double* __restrict__ init,
-                                                                uint8_t* __restrict__ is_new) {
+                                                                uint8_t* __restrict__ is_new,
+                                                                const int64_t* __restrict__ nB_dev) {
     __shared__ int64_t sk[kLookupTile];
     __shared__ int shit[kLookupTile];  // a batch key's table entry relative to a0, or -1 (not in the table)
     const int tid = threadIdx.x;
     const int64_t d0 = (int64_t)blockIdx.x * kLookupTile;
+    nB = dev_count(nB_dev, nB);
+    if (d0 >= nA + nB) return;  // past the device count (a whole block: before any barrier)
     const int64_t d1 = d0 + kLookupTile < nA + nB ? d0 + kLookupTile : nA + nB;
     const int64_t s0 = split[blockIdx.x], s1 = split[blockIdx.x + 1];
     const int64_t a0 = s0, b0 = d0 - a0;
@@ -1026,10 +1036,10 @@ __global__ __launch_bounds__(kFitBlock) void td_fit_pass2_kernel(const int64_t* 
 
 // the tiles' merge-path splits (tiles + 1 of them) into the caller's scratch
 hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t nB, int64_t tile, int64_t tiles,
-                        int64_t* split, hipStream_t stream) {
+                        int64_t* split, hipStream_t stream, const int64_t* nB_dev = nullptr) {
     const int64_t ns = tiles + 1;
     td_splits_kernel<<<(unsigned)((ns + kMergeBlock - 1) / kMergeBlock), kMergeBlock, 0, stream>>>(A, nA, B, nB, tile,
-                                                                                                  ns, split);
+                                                                                                  ns, split, nB_dev);
     return hipGetLastError();
 }
 // the split table's bytes for n merged positions in tiles of `tile` (0 when
@@ -1198,8 +1208,9 @@ int oth_td_fit_moments(const int64_t* keys, const double* values, int64_t n, con
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 
-int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
-                  int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream) {
+static int td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                     int64_t n_upd, const int64_t* n_upd_dev, double* init, uint8_t* is_new, void* temp,
+                     size_t* temp_bytes, void* stream) {
     if (n_old < 0 || n_upd < 0 || !temp_bytes) return OTH_EINVAL;
     const size_t need = split_bytes(n_old, n_upd, kLookupTile);
     if (!temp) {  // size query: no work, no launch
@@ -1213,12 +1224,24 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
     const int64_t n = n_old + n_upd;
     const int64_t tiles = (n + kLookupTile - 1) / kLookupTile;
     int64_t* split = static_cast<int64_t*>(temp);
-    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kLookupTile, tiles, split, (hipStream_t)stream);
+    hipError_t e =
+        merge_splits(old_keys, n_old, upd_keys, n_upd, kLookupTile, tiles, split, (hipStream_t)stream, n_upd_dev);
     if (e != hipSuccess) return -(int)e;
     td_lookup_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(old_keys, old_vals, n_old, upd_keys,
-                                                                              n_upd, split, init, is_new);
+                                                                              n_upd, split, init, is_new, n_upd_dev);
     e = hipGetLastError();
     return e != hipSuccess ? -(int)e : OTH_OK;
+}
+int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                  int64_t n_upd, double* init, uint8_t* is_new, void* temp, size_t* temp_bytes, void* stream) {
+    return td_lookup(old_keys, old_vals, n_old, upd_keys, n_upd, nullptr, init, is_new, temp, temp_bytes, stream);
+}
+int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                      int64_t n_upd_max, const int64_t* n_upd_dev, double* init, uint8_t* is_new, void* temp,
+                      size_t* temp_bytes, void* stream) {
+    if (temp && n_upd_max > 0 && !n_upd_dev) return OTH_EINVAL;
+    return td_lookup(old_keys, old_vals, n_old, upd_keys, n_upd_max, n_upd_dev, init, is_new, temp, temp_bytes,
+                     stream);
 }
 
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,

@@ -38,6 +38,7 @@ a shard on the device instead of a random 50,000-state sample; Redis and the
 pyres fan-out stay out of scope.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -48,6 +49,9 @@ from .params import SHARDS
 
 A = 0.03       # ProgressPositionMovesLearn.a  (progress_position_moves_learn.py:22)
 LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py:24)
+# the lookup queued ahead of the host's read of the segment counts (round 5);
+# OTH_TD_LOOKUP_AHEAD=0 reads them first (tools/diag A/Bs only)
+_LOOKUP_AHEAD = os.environ.get("OTH_TD_LOOKUP_AHEAD", "1") != "0"
 LONG_MIN = 48  # updates per key from which oth_td_ema_split runs the key on a whole wave
 # include/othello.h OTH_TD_KEY layout: each field as wide as its largest value
 # (discs 0..64, moves 0..63, region counts up to the region sizes 4, 8, 4, 8,
@@ -287,10 +291,13 @@ class StateMap:
         self._apply_segments(sv, *segs)
 
     def _segments(self, sorted_in, values):
-        """The sorted stream's segments in one pass pair and one host sync:
-        from keys (oth_td_segments), or (values given) from the sorted packed
-        words, the values written as a side effect (oth_td_segments_words).
-        Returns (ukeys, seg_off, long_idx)."""
+        """The sorted stream's segments in one pass pair: from keys
+        (oth_td_segments), or (values given) from the sorted packed words, the
+        values written as a side effect (oth_td_segments_words).  Returns
+        (ukeys, seg_off, long_idx, counts) sized for every update; counts =
+        (the device pair (n keys, n long keys), its pinned host copy, the
+        copy's event), not yet waited for: _apply_segments queues the lookup
+        behind the segments pass before the host reads them."""
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         n = sorted_in.numel()
@@ -307,22 +314,37 @@ class StateMap:
                                                       seg_off.data_ptr(), ukeys.data_ptr(), long_idx.data_ptr(),
                                                       cnt.data_ptr(), values.data_ptr()), stream, self.device,
                           "oth_td_segments_words")
-        n_upd, n_long = cnt.tolist()
-        return ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
+        host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        host.copy_(cnt, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ukeys, seg_off, long_idx, (cnt, host, ev)
 
-    def _apply_segments(self, sv, ukeys, seg_off, long_idx):
+    def _apply_segments(self, sv, ukeys, seg_off, long_idx, counts):
         """Each key's EMA in stream order over its segment of sv, then the merge."""
+        cnt, host, ev = counts
+        if not _LOOKUP_AHEAD:  # A/B (OTH_TD_LOOKUP_AHEAD=0): the host reads the counts first
+            ev.synchronize()
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         with torch.cuda.device(self.device):
-            n_upd = ukeys.numel()
             pending = None
             if len(self):
-                init = torch.empty(n_upd, dtype=torch.float64, device=self.device)
-                is_new = torch.empty(n_upd, dtype=torch.uint8, device=self.device)
-                _with_scratch(lib.oth_td_lookup, (self.keys.data_ptr(), self.values.data_ptr(), len(self),
-                                                  ukeys.data_ptr(), n_upd, init.data_ptr(), is_new.data_ptr()),
-                              stream, self.device, "oth_td_lookup")
+                # the lookup queued before the host reads the key count: it
+                # takes the count from the device (oth_td_lookup_dev), so the
+                # host's read below overlaps it (round 5: the read and the
+                # Python after it left the GPU idle ~50 us per batch)
+                n_max = ukeys.numel()
+                init = torch.empty(n_max, dtype=torch.float64, device=self.device)
+                is_new = torch.empty(n_max, dtype=torch.uint8, device=self.device)
+                _with_scratch(lib.oth_td_lookup_dev, (self.keys.data_ptr(), self.values.data_ptr(), len(self),
+                                                      ukeys.data_ptr(), n_max, cnt.data_ptr(), init.data_ptr(),
+                                                      is_new.data_ptr()), stream, self.device, "oth_td_lookup_dev")
+            ev.synchronize()  # the counts' copy, queued before the lookup
+            n_upd, n_long = host.tolist()
+            ukeys, seg_off, long_idx = ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
+            if len(self):
+                init, is_new = init[:n_upd], is_new[:n_upd]
                 # the merge's sizes before the EMA: the host reads the new-key
                 # count while the EMA runs (round 5; a stream sync after the
                 # EMA left the GPU idle while the host sized and launched the

@@ -209,6 +209,30 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     assert out_v.h.tolist() == [want[k] for k in sorted(want)]
 
 
+@pytest.mark.parametrize("count", [0, 1, 2047, 2048, 30_000, 50_000, 60_000])
+def test_td_lookup_dev_pair(count):
+    """oth_td_lookup_dev (the batch's key count read from device memory, the
+    arrays and scratch sized for n_upd_max = 50,000) on both builds: the first
+    `count` entries as oth_td_lookup over that many keys, the rest untouched;
+    a count past n_upd_max is clamped to it."""
+    rng = np.random.default_rng(count + 5)
+    old = np.unique(rng.integers(0, 1 << 40, size=40_000, dtype=np.int64))
+    n_max = 50_000
+    upd = np.unique(np.concatenate([rng.choice(old, 20_000, replace=False),
+                                    rng.integers(0, 1 << 40, size=40_000, dtype=np.int64)]))[:n_max]
+    ov = rng.normal(size=len(old))
+    ok, ovb, uk = Buf(old), Buf(ov), Buf(upd)
+    cnt = Buf(np.array([count, 123], np.int64))
+    init, is_new = Buf(np.full(n_max, 9.0)), Buf(np.full(n_max, 7, np.uint8))
+    both_scratch("oth_td_lookup_dev", ok, ovb, len(old), uk, n_max, cnt, init, is_new)
+    same(init, is_new)
+    m = min(count, n_max)
+    olddict = dict(zip(old.tolist(), ov.tolist()))
+    assert init.h[:m].tolist() == [olddict.get(k, 0.0) for k in upd[:m].tolist()]
+    np.testing.assert_array_equal(is_new.h[:m], (~np.isin(upd[:m], old)).astype(np.uint8))
+    assert (init.h[m:] == 9.0).all() and (is_new.h[m:] == 7).all()
+
+
 @pytest.mark.parametrize("shape", ["below", "above", "runs", "tiny_table"])
 def test_td_merge_pair_skewed(shape):
     """Merge-path splits at the extremes (oth_td_lookup / oth_td_merge take
@@ -626,6 +650,10 @@ def test_empty_null_and_invalid_arguments():
         assert lib.oth_td_lookup(None, None, 5, None, 0, None, None, one, ctypes.byref(tb), s) == E  # table w/o pointers
         assert lib.oth_td_lookup(None, None, 0, None, 0, None, None, one, ctypes.byref(tb), s) == 0
         assert lib.oth_td_lookup(None, None, 0, None, 3, None, None, one, ctypes.byref(tb), s) == E
+        # the device-count form: no count pointer with keys to look up
+        assert lib.oth_td_lookup_dev(None, None, 0, one, 3, None, one, one, one, ctypes.byref(tb), s) == E
+        assert lib.oth_td_lookup_dev(None, None, 0, None, -1, one, None, None, one, ctypes.byref(tb), s) == E
+        assert lib.oth_td_lookup_dev(None, None, 10_000, None, 7_000, None, None, None, None, ctypes.byref(tb), s) == 0
         # size queries read nothing but the counts
         assert lib.oth_td_lookup(None, None, 10_000, None, 7_000, None, None, None, ctypes.byref(tb), s) == 0
         assert tb.value >= 8 or lib is not _lib.load()

@@ -17,5 +17,5 @@ from subproc_amd import ops  # noqa: E402
 dev = torch.device("cuda", 0)
 r = bench._bench_td(ops, torch, dev, argparse.Namespace(seed=0x5EED), reps=int(sys.argv[2]) if len(sys.argv) > 2 else 7)
 print("%-14s fork=%s median %.3f ms (%.3f-%.3f)  %.3e updates/s" % (
-    os.path.basename(sys.argv[1]), os.environ.get("OTH_TD_EMA_FORK", "1"), r["ms"], r["ms_min"], r["ms_max"],
+    os.path.basename(sys.argv[1]), os.environ.get("OTH_TD_EMA_FORK", "0"), r["ms"], r["ms_min"], r["ms_max"],
     r["value"]), flush=True)

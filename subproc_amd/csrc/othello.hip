@@ -1988,16 +1988,15 @@ __device__ __forceinline__ int64_t spec_key_of(const SpecPlanEntry* plan, int64_
     return lo;
 }
 // one wave per work item: parts q = 64 c + lane of its key, guesses and end states out
-__global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double* __restrict__ vals,
-                                                                   const int64_t* __restrict__ seg_off,
-                                                                   const double* __restrict__ init, double a,
-                                                                   double oma, const int64_t* __restrict__ hdr,
-                                                                   const SpecPlanEntry* __restrict__ plan,
-                                                                   double* __restrict__ guess,
-                                                                   double* __restrict__ fin, int warm16) {
-    __shared__ SpecWave sh;
+// the parts of block `blk` of `grid` (a grid-stride loop over the work items)
+__device__ __forceinline__ void td_spec_parts_body(int64_t blk, int64_t grid, const double* __restrict__ vals,
+                                                   const int64_t* __restrict__ seg_off,
+                                                   const double* __restrict__ init, double a, double oma,
+                                                   const int64_t* __restrict__ hdr,
+                                                   const SpecPlanEntry* __restrict__ plan, double* __restrict__ guess,
+                                                   double* __restrict__ fin, int warm16, SpecWave& sh) {
     const int64_t n_spec = uniform64(hdr[0]), items = uniform64(hdr[1]);
-    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+    for (int64_t w = blk; w < items; w += grid) {
         const int64_t key = uniform64(spec_key_of(plan, n_spec, w));
         const int64_t s = uniform64(plan[key].s), pb = uniform64(plan[key].part_base);
         const int64_t ib = uniform64(plan[key].item_base), np = uniform64(plan[key].n_parts);
@@ -2013,6 +2012,16 @@ __global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double*
             fin[pb + q] = v;
         }
     }
+}
+__global__ __launch_bounds__(kSpecLanes) void td_spec_parts_kernel(const double* __restrict__ vals,
+                                                                   const int64_t* __restrict__ seg_off,
+                                                                   const double* __restrict__ init, double a,
+                                                                   double oma, const int64_t* __restrict__ hdr,
+                                                                   const SpecPlanEntry* __restrict__ plan,
+                                                                   double* __restrict__ guess,
+                                                                   double* __restrict__ fin, int warm16) {
+    __shared__ SpecWave sh;
+    td_spec_parts_body(blockIdx.x, gridDim.x, vals, seg_off, init, a, oma, hdr, plan, guess, fin, warm16, sh);
 }
 // one wave per split key: its parts checked in order, 64 at a time; missed
 // guesses rerun from their predecessor's end state until all match
@@ -2080,16 +2089,20 @@ inline size_t spec_scratch_bytes(int64_t n_long, int64_t n_values) {
 #endif
 constexpr int kTdStage = OTH_TD_STAGE;         // doubles per LDS stage
 constexpr int kTdStageLoads = kTdStage / 64;   // loads per lane per stage
-__global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ vals,
-                                                         const int64_t* __restrict__ seg_off,
-                                                         const double* __restrict__ init, double a, double oma,
-                                                         double* __restrict__ out,
-                                                         const int64_t* __restrict__ long_idx, int64_t warm) {
-    // (ystage rows padded by one chunk: the chain prefetches the next chunk's y
-    // unconditionally)
-    __shared__ double stage[2][kTdStage], ystage[2][kTdStage + kTdChunk];
+// (ystage rows padded by one chunk: the chain prefetches the next chunk's y
+// unconditionally)
+struct LongStage {
+    double stage[2][kTdStage], ystage[2][kTdStage + kTdChunk];
+};
+__device__ __forceinline__ void td_ema_long_body(int64_t blk, const double* __restrict__ vals,
+                                                 const int64_t* __restrict__ seg_off,
+                                                 const double* __restrict__ init, double a, double oma,
+                                                 double* __restrict__ out, const int64_t* __restrict__ long_idx,
+                                                 int64_t warm, LongStage& ls) {
+    double(&stage)[2][kTdStage] = ls.stage;
+    double(&ystage)[2][kTdStage + kTdChunk] = ls.ystage;
     const int lane = threadIdx.x;
-    const int64_t s = long_idx[blockIdx.x];
+    const int64_t s = long_idx[blk];
     const int64_t b = seg_off[s], e = seg_off[s + 1];
     if (warm > 0 && e - b >= kSpecMinWarms * warm && e - b <= kSpecMaxLen) return;  // a split key (td_spec_*)
     const int64_t n_stage = (e - b + kTdStage - 1) / kTdStage;
@@ -2175,6 +2188,40 @@ __global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restric
         __syncthreads();
     }
     if (lane == 0) out[s] = v;
+}
+__global__ __launch_bounds__(64) void td_ema_long_kernel(const double* __restrict__ vals,
+                                                         const int64_t* __restrict__ seg_off,
+                                                         const double* __restrict__ init, double a, double oma,
+                                                         double* __restrict__ out,
+                                                         const int64_t* __restrict__ long_idx, int64_t warm) {
+    __shared__ LongStage ls;
+    td_ema_long_body(blockIdx.x, vals, seg_off, init, a, oma, out, long_idx, warm, ls);
+}
+// The long keys and the split keys' parts in one launch (late round 5): blocks
+// [0, parts_grid) run the parts (a grid-stride loop over the work items), the
+// rest the long keys; the parts first, so that their few long-running blocks
+// are dispatched at once rather than behind thousands of long keys.  Both are latency-bound chains on
+// few waves; launched one after the other they ran ~90 + ~95 us, side by side
+// about as long as the longer.  One LDS area serves either role.
+union LongOrParts {
+    LongStage ls;
+    SpecWave sw;
+};
+__global__ __launch_bounds__(64) void td_ema_long_parts_kernel(const double* __restrict__ vals,
+                                                               const int64_t* __restrict__ seg_off,
+                                                               const double* __restrict__ init, double a, double oma,
+                                                               double* __restrict__ out,
+                                                               const int64_t* __restrict__ long_idx, int64_t warm,
+                                                               int64_t n_long, const int64_t* __restrict__ hdr,
+                                                               const SpecPlanEntry* __restrict__ plan,
+                                                               double* __restrict__ guess, double* __restrict__ fin,
+                                                               int warm16, int64_t parts_grid) {
+    __shared__ LongOrParts lp;
+    const int64_t blk = blockIdx.x;
+    if (blk < parts_grid)
+        td_spec_parts_body(blk, parts_grid, vals, seg_off, init, a, oma, hdr, plan, guess, fin, warm16, lp.sw);
+    else
+        td_ema_long_body(blk - parts_grid, vals, seg_off, init, a, oma, out, long_idx, warm, lp.ls);
 }
 
 inline int status(hipError_t e) { return e == hipSuccess ? OTH_OK : -(int)e; }
@@ -2606,10 +2653,12 @@ static int64_t td_spec_warm(double oma) {
     return w > (double)(1 << 20) ? 0 : (int64_t)w;
 }
 
-// the split keys: plan, parts (one wave per 64 parts), check and reruns, on stream s
+// the split keys: plan, parts (one wave per 64 parts), check and reruns, on
+// stream s; with_long: the long keys' waves in the parts' launch
+// (td_ema_long_parts_kernel)
 static int td_spec_launch(const double* values, const int64_t* seg_off, const double* init, double a,
                           double one_minus_a, double* out, const int64_t* long_idx, int64_t n_long, int64_t n_values,
-                          int64_t warm, void* temp, hipStream_t s) {
+                          int64_t warm, void* temp, hipStream_t s, bool with_long) {
     int64_t* hdr = static_cast<int64_t*>(temp);
     SpecPlanEntry* plan = reinterpret_cast<SpecPlanEntry*>(hdr + kSpecHdr);
     double* guess = reinterpret_cast<double*>(plan + std::max<int64_t>(n_long, 1));
@@ -2626,8 +2675,13 @@ static int td_spec_launch(const double* values, const int64_t* seg_off, const do
     rc = launched();
     if (rc != OTH_OK) return rc;
     const int64_t items = std::min<int64_t>(parts / kSpecLanes + n_long, 1024);
-    td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, s>>>(values, seg_off, init, a, one_minus_a, hdr, plan, guess,
-                                                                 fin, warm16);
+    if (with_long)
+        td_ema_long_parts_kernel<<<(unsigned)(n_long + items), 64, 0, s>>>(values, seg_off, init, a, one_minus_a, out,
+                                                                            long_idx, warm, n_long, hdr, plan, guess,
+                                                                            fin, warm16, items);
+    else
+        td_spec_parts_kernel<<<(unsigned)items, kSpecLanes, 0, s>>>(values, seg_off, init, a, one_minus_a, hdr, plan,
+                                                                     guess, fin, warm16);
     rc = launched();
     if (rc != OTH_OK) return rc;
     td_spec_fix_kernel<<<(unsigned)std::min<int64_t>(n_long, 256), kSpecLanes, 0, s>>>(values, seg_off, init, a,
@@ -2657,14 +2711,18 @@ int oth_td_ema_split(const double* values, const int64_t* seg_off, const double*
     const hipStream_t s = (hipStream_t)stream;
     TdFork fork(s, n_long == 0 ? 0 : (warm > 0 ? 2 : 1));
     if (fork.rc != OTH_OK) return fork.rc;
+    // on one stream (no fork), the long keys share the split keys' parts
+    // launch (OTH_TD_EMA_MERGED=0 in the environment: separate launches, A/B)
+    static const int merged_ok = env_int("OTH_TD_EMA_MERGED", 1);
+    const bool split = n_long > 0 && warm > 0, merged = split && fork.n == 0 && merged_ok;
     int rc = OTH_OK;
-    if (n_long > 0) {
+    if (n_long > 0 && !merged) {
         td_ema_long_kernel<<<(unsigned)n_long, 64, 0, fork.side(0)>>>(values, seg_off, init, a, one_minus_a, out,
                                                                        long_idx, warm);
         rc = launched();
     }
-    if (rc == OTH_OK && n_long > 0 && warm > 0) rc = td_spec_launch(values, seg_off, init, a, one_minus_a, out, long_idx,
-                                                                    n_long, n_values, warm, temp, fork.side(1));
+    if (rc == OTH_OK && split) rc = td_spec_launch(values, seg_off, init, a, one_minus_a, out, long_idx, n_long,
+                                                   n_values, warm, temp, fork.side(1), merged);
     if (rc != OTH_OK) return fork.join(rc);
     if (long_min <= 3 * kTdChunk)
         td_ema_kernel<true><<<blocks_for(n_seg), kBlock, 0, s>>>(values, seg_off, init, a, one_minus_a, out, n_seg,

@@ -171,3 +171,50 @@ def test_fit_on_device_matches_sklearn():
         np.testing.assert_allclose(coef[k], lr.coef_, rtol=1e-6, atol=1e-9)  # float64 normal equations vs SVD
     w = params.from_coef(coef)
     assert w.dtype == np.int8 and np.abs(w).max() == 127
+
+
+_EMA_PROBE = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from subproc_amd import _lib, td
+a, oma = 0.03, 0.97
+rng = np.random.default_rng(9)
+lengths = [1, 47, 48, 600, 5825, 5826, 9000, 70001]
+vals, seg = [], [0]
+for L in lengths:
+    vals += (rng.normal(size=L) * 0.01).tolist()
+    seg.append(len(vals))
+dv = torch.tensor(vals, dtype=torch.float64, device="cuda")
+ds = torch.tensor(seg, dtype=torch.int64, device="cuda")
+init = torch.full((len(lengths),), 0.5, dtype=torch.float64, device="cuda")
+out = torch.empty(len(lengths), dtype=torch.float64, device="cuda")
+li = torch.tensor([i for i, L in enumerate(lengths) if L >= 48], dtype=torch.int64, device="cuda")
+td._with_scratch(_lib.load().oth_td_ema_split, (dv.data_ptr(), ds.data_ptr(), init.data_ptr(), a, oma,
+                                                out.data_ptr(), len(lengths), 48, li.data_ptr(), li.numel(),
+                                                dv.numel()), torch.cuda.current_stream().cuda_stream, "cuda", "ema")
+want = []
+for k, L in enumerate(lengths):
+    v = 0.5
+    for x in vals[seg[k]:seg[k + 1]]:
+        v = x if v == 0.0 else v * oma + x * a
+    want.append(v)
+assert out.cpu().tolist() == want, "EMA differs"
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"OTH_TD_EMA_FORK": "1"}, {"OTH_TD_EMA_MERGED": "0"}, {}])
+def test_td_ema_split_launch_variants(env):
+    """oth_td_ema_split's launch schedules, each read once per process from the
+    environment, in a child process: the side-stream fork (OTH_TD_EMA_FORK=1,
+    opt-in), the long keys and split-key parts as separate launches
+    (OTH_TD_EMA_MERGED=0), and the default (one launch for both).  Short,
+    long, unsplit-long and split keys in one call, bit for bit the sequential
+    rule at the learner's rate."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _EMA_PROBE, root], env={**os.environ, **env}, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr

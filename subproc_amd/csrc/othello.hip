@@ -592,7 +592,9 @@ static_assert(sizeof(Parked) == 32, "two 16-B LDS accesses per parked game");
 constexpr u64 kParkedGame = ~0ull;
 
 #ifdef OTH_DIAG
-__device__ unsigned long long* g_diag;  // per wave: start, end (s_memrealtime), hw_id, iterations
+// per wave: start, end (s_memrealtime), hw_id, and (random policy) the wave's
+// issued plies (executions of the ply step) << 32 | its lanes' plies
+__device__ unsigned long long* g_diag;
 #endif
 
 // Move records of the random policy (RECORD): a lane's record is one 128-byte
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
     RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
 #ifdef OTH_DIAG
     const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long diag_iters = 0;
+    unsigned long long diag_iters = 0, diag_wave_iters = 0;
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
 #endif
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
@@ -761,7 +763,8 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
             // ended, ~7 times per batch.
             auto ply_of = [&](u64& X, u64& Y) -> bool {
 #ifdef OTH_DIAG
-                diag_iters++;
+                diag_iters++;  // this lane's plies
+                if ((u32)lane == (u32)__builtin_amdgcn_readfirstlane(lane)) diag_wave_iters++;  // the wave's
 #endif
                 Position pos;
                 analyse<kRandomFillOrder>(X, Y, pos);
@@ -935,6 +938,10 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
     }
 
 #ifdef OTH_DIAG
+    for (int off = 32; off >= 1; off >>= 1) {
+        diag_iters += __shfl_xor(diag_iters, off);
+        diag_wave_iters += __shfl_xor(diag_wave_iters, off);
+    }
     if (lane == 0 && g_diag) {
         unsigned hwid;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
@@ -944,7 +951,7 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
         d[0] = diag_t0;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = ((unsigned long long)xcc << 32) | hwid;
-        d[3] = diag_iters;
+        d[3] = (diag_wave_iters << 32) | (diag_iters & 0xffffffffull);
     }
 #endif
     // plies: wave reduction, one LDS atomic per wave

@@ -31,9 +31,11 @@ int main(int argc, char** argv) {
         std::vector<double> lifes;
         for (long long w = 0; w < maxw; w++) { if (!d[4*w+1]) continue; waves++; t0 = std::min(t0, d[4*w]); t1 = std::max(t1, d[4*w+1]); }
         std::vector<double> starts, ends;
-        for (long long w = 0; w < maxw; w++) { if (!d[4*w+1]) continue; double l = (d[4*w+1]-d[4*w]) / 100.0; life += l; lifes.push_back(l); it += d[4*w+3]; maxit = std::max(maxit, d[4*w+3]); minit = std::min(minit, d[4*w+3]); starts.push_back((d[4*w]-t0)/100.0); ends.push_back((d[4*w+1]-t0)/100.0);}
+        double issued = 0, useful = 0;
+        for (long long w = 0; w < maxw; w++) { if (!d[4*w+1]) continue; double l = (d[4*w+1]-d[4*w]) / 100.0; life += l; lifes.push_back(l); const unsigned long long wi = d[4*w+3] >> 32, li = d[4*w+3] & 0xffffffffull; issued += 64.0 * wi; useful += li; it += wi; maxit = std::max(maxit, wi); minit = std::min(minit, wi); starts.push_back((d[4*w]-t0)/100.0); ends.push_back((d[4*w+1]-t0)/100.0);}
+        printf("lane-plies: issued %.0f (64 x the waves' ply steps), useful %.0f (the lanes' own), idle %.2f%%\n", issued, useful, 100.0 * (1.0 - useful / issued));
         std::sort(lifes.begin(), lifes.end()); std::sort(starts.begin(), starts.end()); std::sort(ends.begin(), ends.end());
-        printf("n=%lld status=%d ms=%.3f env-steps=%lld -> %.3e steps/s | waves=%lld span_us=%.1f life_us avg=%.1f p5=%.1f p50=%.1f p95=%.1f max=%.1f | start_us p50=%.1f p95=%.1f max=%.1f | end_us p5=%.1f p50=%.1f | iters avg=%.1f min=%llu max=%llu\n",
+        printf("n=%lld status=%d ms=%.3f env-steps=%lld -> %.3e steps/s | waves=%lld span_us=%.1f life_us avg=%.1f p5=%.1f p50=%.1f p95=%.1f max=%.1f | start_us p50=%.1f p95=%.1f max=%.1f | end_us p5=%.1f p50=%.1f | wave ply steps avg=%.1f min=%llu max=%llu\n",
                n, st, ms, h[132], h[132] / (ms * 1e-3), waves, (t1 - t0) / 100.0, life / waves, lifes[waves*5/100], lifes[waves/2], lifes[waves*95/100], lifes.back(), starts[waves/2], starts[waves*95/100], starts.back(), ends[waves*5/100], ends[waves/2], it / waves, minit, maxit);
     }
     return 0;

@@ -465,6 +465,16 @@ int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
                  double* out_vals, void* temp, size_t* temp_bytes, void* stream);
+/* oth_td_merge without its own scratch: lookup_temp is the temp of an
+ * oth_td_lookup / oth_td_lookup_dev call over the same old_keys and
+ * upd_keys (for _dev, with *n_upd_dev == n_upd), queued before this call
+ * and not reused since.  The lookup and the merge cut the merged sequence
+ * into the same tiles, so the lookup's scratch already holds the merge path's
+ * splits: the GPU build reads them instead of searching again (round 5).
+ * The host build ignores lookup_temp.  Same output as oth_td_merge. */
+int oth_td_merge_after_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                              const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                              double* out_vals, const void* lookup_temp, void* stream);
 
 #ifdef __cplusplus
 }

@@ -585,6 +585,16 @@ int oth_td_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old
     return OTH_OK;
 }
 
+/* the host merge needs no splits: lookup_temp is only checked for presence */
+int oth_td_merge_after_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                              const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                              double* out_vals, const void* lookup_temp, void* stream) {
+    size_t zero = 0;
+    if (n_upd > 0 && !lookup_temp) return OTH_EINVAL;
+    return oth_td_merge(old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals,
+                        (void*)&zero, &zero, stream);
+}
+
 /* the count from (host) memory, clamped as the GPU build clamps it */
 int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                       int64_t n_upd_max, const int64_t* n_upd_dev, double* init, uint8_t* is_new, void* temp,

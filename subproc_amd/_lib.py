@@ -64,6 +64,7 @@ SIGNATURES = {
     "oth_td_merge": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup_dev": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "oth_td_merge_after_lookup": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "oth_td_fit_moments": (_I, [_P, _P, _I64, _P, _P, _P]),
 }
 

@@ -1244,6 +1244,34 @@ int oth_td_lookup_dev(const int64_t* old_keys, const double* old_vals, int64_t n
                      stream);
 }
 
+// split_ready: the merge path's splits already in place (a preceding lookup's
+// scratch, oth_td_merge_after_lookup); else computed into temp
+static int td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                    const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                    double* out_vals, void* temp, const int64_t* split_ready, void* stream) {
+    const int64_t n = n_old + n_upd;
+    if (n == 0) return OTH_OK;
+    if (n_upd == 0) {  // the table unchanged (new_before may be NULL: the kernel reads it)
+        hipError_t e = hipMemcpyAsync(out_keys, old_keys, (size_t)n_old * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                                      (hipStream_t)stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_vals, old_vals, (size_t)n_old * sizeof(double), hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream);
+        return e == hipSuccess ? OTH_OK : -(int)e;
+    }
+    const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
+    const int64_t* split = split_ready;
+    if (!split) {
+        int64_t* s = static_cast<int64_t*>(temp);
+        const hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kMergeTile, tiles, s, (hipStream_t)stream);
+        if (e != hipSuccess) return -(int)e;
+        split = s;
+    }
+    td_merge_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(
+        old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, split, out_keys, out_vals);
+    const hipError_t e = hipGetLastError();
+    return e != hipSuccess ? -(int)e : OTH_OK;
+}
 int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                  const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
                  double* out_vals, void* temp, size_t* temp_bytes, void* stream) {
@@ -1256,24 +1284,20 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
     if ((n_old > 0 && (!old_keys || !old_vals)) || (n_upd > 0 && (!upd_keys || !upd_vals || !new_before)) ||
         (n_old + n_upd > 0 && (!out_keys || !out_vals)) || *temp_bytes < need)
         return OTH_EINVAL;
-    const int64_t n = n_old + n_upd;
-    if (n == 0) return OTH_OK;
-    if (n_upd == 0) {  // the table unchanged (new_before may be NULL: the kernel reads it)
-        hipError_t e = hipMemcpyAsync(out_keys, old_keys, (size_t)n_old * sizeof(int64_t), hipMemcpyDeviceToDevice,
-                                      (hipStream_t)stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(out_vals, old_vals, (size_t)n_old * sizeof(double), hipMemcpyDeviceToDevice,
-                               (hipStream_t)stream);
-        return e == hipSuccess ? OTH_OK : -(int)e;
-    }
-    const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
-    int64_t* split = static_cast<int64_t*>(temp);
-    hipError_t e = merge_splits(old_keys, n_old, upd_keys, n_upd, kMergeTile, tiles, split, (hipStream_t)stream);
-    if (e != hipSuccess) return -(int)e;
-    td_merge_kernel<<<(unsigned)tiles, kMergeBlock, 0, (hipStream_t)stream>>>(
-        old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, split, out_keys, out_vals);
-    e = hipGetLastError();
-    return e != hipSuccess ? -(int)e : OTH_OK;
+    return td_merge(old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals, temp,
+                    nullptr, stream);
+}
+// the lookup's tiles are the merge's, so its scratch holds the merge's splits
+int oth_td_merge_after_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
+                              const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
+                              double* out_vals, const void* lookup_temp, void* stream) {
+    if (kMergeTile != kLookupTile) return OTH_EINVAL;  // (an A/B build's OTH_MERGE_K)
+    if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
+        (n_upd > 0 && (!upd_keys || !upd_vals || !new_before || !lookup_temp)) ||
+        (n_old + n_upd > 0 && (!out_keys || !out_vals)))
+        return OTH_EINVAL;
+    return td_merge(old_keys, old_vals, n_old, upd_keys, upd_vals, new_before, n_upd, out_keys, out_vals, nullptr,
+                    static_cast<const int64_t*>(lookup_temp), stream);
 }
 
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,

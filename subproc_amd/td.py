@@ -52,6 +52,9 @@ LAMBDA = 0.90  # ProgressPositionMovesLearn.l  (progress_position_moves_learn.py
 # the lookup queued ahead of the host's read of the segment counts (round 5);
 # OTH_TD_LOOKUP_AHEAD=0 reads them first (tools/diag A/Bs only)
 _LOOKUP_AHEAD = os.environ.get("OTH_TD_LOOKUP_AHEAD", "1") != "0"
+# the merge reads the lookup's merge-path splits (round 5); OTH_TD_MERGE_SPLITS=0
+# searches again (oth_td_merge; A/Bs only)
+_MERGE_SPLITS_FROM_LOOKUP = os.environ.get("OTH_TD_MERGE_SPLITS", "1") != "0"
 LONG_MIN = 48  # updates per key from which oth_td_ema_split runs the key on a whole wave
 # include/othello.h OTH_TD_KEY layout: each field as wide as its largest value
 # (discs 0..64, moves 0..63, region counts up to the region sizes 4, 8, 4, 8,
@@ -158,6 +161,7 @@ def _with_scratch(fn, args, stream, device, what):
     check(fn(*args, None, ctypes.byref(tb), stream), what + " (size query)")
     temp = torch.empty(max(tb.value, 1), dtype=torch.uint8, device=device)
     check(fn(*args, temp.data_ptr(), ctypes.byref(tb), stream), what)
+    return temp
 
 
 class StateMap:
@@ -337,9 +341,12 @@ class StateMap:
                 n_max = ukeys.numel()
                 init = torch.empty(n_max, dtype=torch.float64, device=self.device)
                 is_new = torch.empty(n_max, dtype=torch.uint8, device=self.device)
-                _with_scratch(lib.oth_td_lookup_dev, (self.keys.data_ptr(), self.values.data_ptr(), len(self),
-                                                      ukeys.data_ptr(), n_max, cnt.data_ptr(), init.data_ptr(),
-                                                      is_new.data_ptr()), stream, self.device, "oth_td_lookup_dev")
+                # (its scratch, the merge path's splits, is the merge's too:
+                # oth_td_merge_after_lookup)
+                lk_temp = _with_scratch(lib.oth_td_lookup_dev, (self.keys.data_ptr(), self.values.data_ptr(),
+                                                                len(self), ukeys.data_ptr(), n_max, cnt.data_ptr(),
+                                                                init.data_ptr(), is_new.data_ptr()),
+                                        stream, self.device, "oth_td_lookup_dev")
             ev.synchronize()  # the counts' copy, queued before the lookup
             n_upd, n_long = host.tolist()
             ukeys, seg_off, long_idx = ukeys[:n_upd], seg_off[:n_upd + 1], long_idx[:n_long]
@@ -349,7 +356,7 @@ class StateMap:
                 # count while the EMA runs (round 5; a stream sync after the
                 # EMA left the GPU idle while the host sized and launched the
                 # merge)
-                pending = self._new_before(is_new, lib, stream)
+                pending = self._new_before(is_new, lib, stream) + (lk_temp,)
             else:
                 init = torch.zeros(n_upd, dtype=torch.float64, device=self.device)
             out = torch.empty_like(init)
@@ -383,15 +390,21 @@ class StateMap:
         oth_td_merge (HIP merge path) writes the sorted union, placing every
         element by rank; new_before[j] = batch keys before j that are absent
         from the table (pending: _new_before's result)."""
-        new_before, host, ev = pending
+        new_before, host, ev, lk_temp = pending
         n_old, n_upd = len(self), ukeys.numel()
         ev.synchronize()
         n_new = int(host[0])
         keys = torch.empty(n_old + n_new, dtype=torch.int64, device=self.device)
         vals = torch.empty(n_old + n_new, dtype=torch.float64, device=self.device)
-        _with_scratch(lib.oth_td_merge, (self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(),
-                                         out.data_ptr(), new_before.data_ptr(), n_upd, keys.data_ptr(), vals.data_ptr()),
-                      stream, self.device, "oth_td_merge")
+        if _MERGE_SPLITS_FROM_LOOKUP:  # the lookup's splits (same tiles): no second search
+            check(lib.oth_td_merge_after_lookup(self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(),
+                                                out.data_ptr(), new_before.data_ptr(), n_upd, keys.data_ptr(),
+                                                vals.data_ptr(), lk_temp.data_ptr(), stream),
+                  "oth_td_merge_after_lookup")
+        else:
+            _with_scratch(lib.oth_td_merge, (self.keys.data_ptr(), self.values.data_ptr(), n_old, ukeys.data_ptr(),
+                                             out.data_ptr(), new_before.data_ptr(), n_upd, keys.data_ptr(),
+                                             vals.data_ptr()), stream, self.device, "oth_td_merge")
         self.keys, self.values = keys, vals
 
     def update_from_books(self, books):

@@ -209,6 +209,55 @@ def test_td_merge_pair(n_old, n_upd, overlap):
     assert out_v.h.tolist() == [want[k] for k in sorted(want)]
 
 
+@pytest.mark.parametrize("n_old,n_upd,dev_count", [(40_000, 20_000, None), (40_000, 20_000, 13_001), (1, 5000, None),
+                                                   (5000, 1, 1), (100_000, 70_000, 2048)])
+def test_td_merge_after_lookup_pair(n_old, n_upd, dev_count):
+    """oth_td_merge_after_lookup (the merge reading the merge-path splits a
+    lookup left in its scratch; dev_count: the lookup was oth_td_lookup_dev
+    with that device count over buffers sized for n_upd) on both builds: the
+    same table as oth_td_merge, bit for bit."""
+    rng = np.random.default_rng(n_old + 3 * n_upd)
+    old = np.unique(rng.integers(0, 1 << 40, size=n_old, dtype=np.int64))
+    upd = np.unique(np.concatenate([rng.choice(old, min(len(old), n_upd // 2), replace=False),
+                                    rng.integers(0, 1 << 40, size=n_upd, dtype=np.int64)]))[:n_upd]
+    m = len(upd) if dev_count is None else dev_count
+    ov, uv = rng.normal(size=len(old)), rng.normal(size=len(upd))
+    new = ~np.isin(upd[:m], old)
+    nb = np.concatenate([[0], np.cumsum(new)]).astype(np.int64)
+    n_out = len(old) + int(nb[-1])
+    want = dict(zip(old.tolist(), ov.tolist()))
+    want.update(zip(upd[:m].tolist(), uv[:m].tolist()))
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    st = torch.cuda.current_stream().cuda_stream
+    ok, ovb, uk, uvb, nbb = Buf(old), Buf(ov), Buf(upd), Buf(uv), Buf(nb)
+    init, is_new = Buf(np.zeros(len(upd))), Buf(np.zeros(len(upd), np.uint8))
+    cnt = Buf(np.array([m], np.int64))
+    for lib, ptr, s in ((cpu, lambda b: HOSTP(b.h), None), (gpu, lambda b: b.d.data_ptr(), st)):
+        tb = ctypes.c_size_t(0)
+        if dev_count is None:
+            args = (ptr(ok), ptr(ovb), len(old), ptr(uk), m, ptr(init), ptr(is_new))
+            fn = lib.oth_td_lookup
+        else:
+            args = (ptr(ok), ptr(ovb), len(old), ptr(uk), len(upd), ptr(cnt), ptr(init), ptr(is_new))
+            fn = lib.oth_td_lookup_dev
+        assert fn(*args, None, ctypes.byref(tb), s) == 0
+        temp = (torch.empty(max(tb.value, 1), dtype=torch.uint8, device=DEV) if lib is gpu
+                else np.zeros(max(tb.value, 1), np.uint8))
+        tp = temp.data_ptr() if lib is gpu else HOSTP(temp)
+        assert fn(*args, tp, ctypes.byref(tb), s) == 0
+        out_k, out_v = (np.full(n_out, -7, np.int64), np.zeros(n_out)) if lib is cpu else \
+            (torch.full((n_out,), -7, dtype=torch.int64, device=DEV), torch.zeros(n_out, dtype=torch.float64, device=DEV))
+        okp = HOSTP(out_k) if lib is cpu else out_k.data_ptr()
+        ovp = HOSTP(out_v) if lib is cpu else out_v.data_ptr()
+        assert lib.oth_td_merge_after_lookup(ptr(ok), ptr(ovb), len(old), ptr(uk), ptr(uvb), ptr(nbb), m, okp, ovp,
+                                             tp, s) == 0
+        if lib is gpu:
+            torch.cuda.synchronize()
+            out_k, out_v = out_k.cpu().numpy(), out_v.cpu().numpy()
+        assert out_k.tolist() == sorted(want)
+        assert out_v.tolist() == [want[k] for k in sorted(want)]
+
+
 @pytest.mark.parametrize("count", [0, 1, 2047, 2048, 30_000, 50_000, 60_000])
 def test_td_lookup_dev_pair(count):
     """oth_td_lookup_dev (the batch's key count read from device memory, the

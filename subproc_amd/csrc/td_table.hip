@@ -1047,13 +1047,19 @@ hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t 
 // ---- segments of the key-sorted update stream (oth_td_segments): where
 // torch's unique_consecutive + cumsum + nonzero took ~0.37 ms per 32M
 // updates (a reduce-by-key, a scan, a partition and their fills, and two
-// host syncs), one wave streams 1,024 keys in 16 coalesced rounds of 64: a
+// host syncs), one wave streams 512 keys in 8 coalesced rounds of 64: a
 // segment starts where a key differs from the one before (the lane's
 // neighbour by a DPP shift, the round's first from the round before), a
 // ballot and mbcnt place the starts.  A count pass and a write pass around a
 // scan of the waves' counts (rocPRIM) keep the order; the long segments the
 // same way, by a second ballot and scan.
-constexpr int kSegRounds = 16;
+// rounds of 64 words per wave: 8 (late round 5; tools/diag/td_ab.sh, two
+// passes, count / write pass per 32.2M words: 4 rounds 78 / 137 us, 6: 75 /
+// 134, 8: 71 / 133, 16: 79 / 137, 32: 103 / 153)
+#ifndef OTH_SEG_ROUNDS  // A/B builds
+#define OTH_SEG_ROUNDS 8
+#endif
+constexpr int kSegRounds = OTH_SEG_ROUNDS;
 constexpr int kSegWaveKeys = 64 * kSegRounds;
 constexpr int kSegBlock = 256;
 constexpr int kSegWavesPerBlock = kSegBlock / 64;
@@ -1085,7 +1091,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
     const int64_t w = (int64_t)blockIdx.x * kSegWavesPerBlock + (threadIdx.x >> 6);
     const int64_t base = w * kSegWaveKeys;
     if (base >= n) return;  // wave-uniform
-    // every round's key loaded before the first is used (17 loads in flight:
+    // every round's key loaded before the first is used (kSegRounds + 1 loads in flight:
     // k[kSegRounds] is the next wave's first round)
     int64_t k[kSegRounds + 1];
     uint32_t payload[kSegRounds];  // WORDS, WRITE: the word's top 28 bits

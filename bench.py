@@ -27,7 +27,8 @@ Also reported on rank 0 (secondary, same JSON line):
     sample of the same workload on the host cores.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload rollout|greedy|step]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+Multi-GPU: python bench.py --gpus N ... (starts N rank processes itself), or
+           python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
@@ -142,8 +143,63 @@ def parse():
     return p.parse_args()
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, cmd, env=None, port=None, poll_s=0.2):
+    """Start `n` ranks of `cmd` as child processes (one per GPU, the layout
+    torch.distributed.run gives) with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set, and wait for them.  The children inherit
+    stdout, so rank 0's JSON line is the line this process prints.  Returns 0
+    if every rank exits 0; otherwise the first failing rank's code (a signal
+    death maps to 128 + signal), after ending the remaining ranks, whose
+    collectives could no longer complete.  The caller must not have touched
+    the GPU: the children are fresh processes, never an exec.  This is the
+    fan-out the reference does with replearn.py:78-86 -> eljem_worker.py:10."""
+    import signal
+    import subprocess
+
+    base = dict(os.environ if env is None else env)
+    port = port or free_port()
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=e, start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for q in live:  # the exact children this call started
+                        os.killpg(q.pid, signal.SIGTERM)
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without torchrun: this process stays off the
+        # GPU and runs N ranks of the same command line as child processes
+        raise SystemExit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]))
     if args.lib:
         from subproc_amd import _lib
         _lib.LIB_PATH = os.path.abspath(args.lib)
@@ -712,7 +768,11 @@ def _cpu_baseline(args, workload):
     # environment sets it (the GPU box sets 16: its CPU share per GPU)
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = max(1, min(affinity, int(omp))) if omp and omp.isdigit() else affinity
-    host = {"nproc": os.cpu_count(), "affinity_cores": affinity, "omp_num_threads": omp}
+    host = {"nproc": os.cpu_count(), "affinity_cores": affinity, "omp_num_threads": omp,
+            "cores_note": "threads = min(affinity cores, OMP_NUM_THREADS): the GPU box's affinity mask shows the "
+                          "whole host (%d cores) but its CPU share per GPU is OMP_NUM_THREADS=%s, which the pool "
+                          "sets and asks jobs to stay within; the one_thread figure scales the port per core"
+                          % (affinity, omp)}
     if workload == "step":
         pos = oracle.sample_midgame(65536, args.seed)
         t0 = time.perf_counter()

@@ -109,3 +109,22 @@ def test_bench_two_ranks_line_the_driver_parses():
     assert set(sec) == {"step_steady_16M", "step_65536"}
     for name in sec:
         assert sec[name]["n_gpus"] == 2 and sec[name]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_plain_command():
+    """Exactly `python bench.py --gpus 2 --steps 3 --warmup 1` (no torchrun: the
+    bench starts its two ranks itself), both ranks on this box's one GPU with
+    the collectives over gloo: one line, n_gpus 2, every game counted once."""
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert REQUIRED <= set(out)
+    assert out["n_gpus"] == 2 and out["config"]["world_size"] == 2
+    assert out["config"]["games_counted"] == 2 * 3 * (1 << 20)

@@ -438,6 +438,18 @@ def test_config4_global_histogram_equals_shards():
     assert int(whole.hist[:129].sum()) == 8 * n
 
 
+def test_config4_histogram_vs_oracle():
+    """The config-4 global histogram (8,388,608 random games, seed 0x5EED, ids
+    0..8M-1: what the 8 ranks' RCCL all-reduce sums to) against the oracle
+    playing the same 8M games on all host threads (~40 s of 16 threads on the
+    GPU box).  Rule: game_runner.py:165-201 / board.py:192-209; the result rule
+    of game_runner.py:194-199 fills bins 129-131."""
+    n = 8 << 20
+    whole = ops.rollout(n, 0x5EED, 0, device=DEV, want_boards=False, want_diff=False, want_plies=False)
+    o = oracle.rollout(n, 0x5EED, 0, policy=0, n_random=10, n_threads=0)
+    np.testing.assert_array_equal(whole.hist.cpu().numpy(), o["hist"])
+
+
 def test_rollout_match_vs_oracle_and_equal_tables():
     from subproc_amd.params import DEFAULT_WEIGHTS
     n = 4096

@@ -353,8 +353,8 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
                           const int64_t* base, uint64_t* words, int64_t n, void* stream);
 /* Stable sort of n packed words by bits 0..OTH_TD_SKEY_BITS-1 (the skey):
  * equal keys keep their stream order; words_out distinct from words_in.
- * temp / temp_bytes as oth_td_sort_pairs.  (The build's own LSD radix sort,
- * round 5; round 4 called rocPRIM's.) */
+ * temp / temp_bytes as oth_td_sort_pairs.  (rocPRIM's onesweep radix sort,
+ * 4 passes of 9 bits: the one vendor kernel of the library, DESIGN.md.) */
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream);
 /* oth_td_sort_packed followed by oth_td_unpack in one: the sorted words'
@@ -398,6 +398,14 @@ int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, voi
  * so words not made by oth_td_updates_packed never read past lam_pow. */
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                   void* stream);
+
+/* The number of packed words whose turn_left exceeded the lam_pow table
+ * (clamped, as above) that oth_td_unpack, oth_td_sort_unpack and
+ * oth_td_segments_words have read on the current device since the last reset
+ * (a device-side counter): 0 for every word array oth_td_updates_packed
+ * wrote.  *count (host memory) receives it once the work queued on `stream`
+ * so far is done (the call synchronizes the stream); reset != 0 zeroes it. */
+int oth_td_word_errors(uint64_t* count, int reset, void* stream);
 
 /* The grouping sort between oth_td_updates and oth_td_ema: the n (key, value)
  * pairs of the update stream into key order, stable (a key's values keep

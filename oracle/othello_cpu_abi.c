@@ -315,10 +315,22 @@ int oth_td_updates_packed(const uint64_t* pos_boards, const int64_t* row_off, co
     return OTH_OK;
 }
 
-/* turn_left as a lam_pow index, clamped to the table (as the GPU build) */
+/* turn_left as a lam_pow index, clamped to the table and counted when out of
+ * range (as the GPU build) */
+static uint64_t g_td_bad_words;
 static uint64_t td_turn_idx(uint64_t w) {
     const uint64_t t = (w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK;
-    return t < OTH_POS_STRIDE - 1 ? t : OTH_POS_STRIDE - 1;
+    if (t < OTH_POS_STRIDE) return t;
+    g_td_bad_words++;
+    return OTH_POS_STRIDE - 1;
+}
+
+int oth_td_word_errors(uint64_t* count, int reset, void* stream) {
+    (void)stream;
+    if (!count) return OTH_EINVAL;
+    *count = g_td_bad_words;
+    if (reset) g_td_bad_words = 0;
+    return OTH_OK;
 }
 
 int oth_td_unpack(const uint64_t* words, const double* lam_pow, int64_t* keys, double* values, int64_t n,

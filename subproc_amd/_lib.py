@@ -61,6 +61,7 @@ SIGNATURES = {
     "oth_td_sort_packed": (_I, [_P, _P, _I64, _P, _P, _P]),
     "oth_td_sort_unpack": (_I, [_P, _P, _P, _P, _I64, _P, _P, _P]),
     "oth_td_unpack": (_I, [_P, _P, _P, _P, _I64, _P]),
+    "oth_td_word_errors": (_I, [_P, _I, _P]),
     "oth_td_merge": (_I, [_P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "oth_td_lookup_dev": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),

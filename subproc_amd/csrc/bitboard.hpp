@@ -178,10 +178,8 @@ struct Position {
 // instead of 2.5, and the bit pairs of 64-bit values make that likely; the
 // order with the fewest such instructions in each kernel's hot loop was picked
 // by tools/valu_mix.py (random rollout: 7-9-8, 11 -> 3 per ply).
-#ifndef OTH_FILL_ORDER
-#define OTH_FILL_ORDER 798
-#endif
-template <int ORDER = OTH_FILL_ORDER>
+constexpr int kFillOrder = 798;
+template <int ORDER = kFillOrder>
 __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
     const u64 Oi = and2(O, INNER_FILES);
     s.Oi = Oi;
@@ -230,13 +228,6 @@ __device__ __forceinline__ void analyse(u64 P, u64 O, Position& s) {
 // bit-reversed board.  Table rows: 0..2 = rays +8, +9, +7 (normal order),
 // 3..5 = rays -8, -9, -7 stored bit-reversed; 64 squares each (3 KiB).
 constexpr int kRayRows = 6;
-// OTH_FLIPS_NORMAL_DEC (A/B builds only, round 4): the three decreasing rays'
-// flips in normal orientation, by the ray's highest non-run square (v_ffbh),
-// instead of on the bit-reversed board; table rows 3..5 then hold the rays
-// in normal orientation and the run sets keep A2 / A4 / A6 unreversed
-#ifndef OTH_FLIPS_NORMAL_DEC
-#define OTH_FLIPS_NORMAL_DEC 0
-#endif
 // the LDS table adds two rows per square: 6 = the square's bit, 7 = its bit
 // on the reversed board (1 << (63 - sq)); read with the rays, they replace two
 // variable 64-bit shifts of the VALU-bound loop by LDS reads
@@ -261,7 +252,7 @@ __device__ __forceinline__ void ray_table_init(u64* tab) {
             continue;
         }
         const u64 r = ray_from(sq, dx[row], dy[row]);
-        tab[e] = (row < 3 || OTH_FLIPS_NORMAL_DEC) ? r : rev64(r);
+        tab[e] = row < 3 ? r : rev64(r);
     }
 }
 // the move's bit from the table (row kRayRows)
@@ -286,21 +277,7 @@ struct RunSets {
     u64 A1, A3, A5, A7, rA0, rA2, rA4, rA6;
 };
 __device__ __forceinline__ RunSets run_sets(const Position& s) {
-#if OTH_FLIPS_NORMAL_DEC
-    return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), s.A[2], s.A[4], s.A[6]};
-#else
     return RunSets{s.A[1], s.A[3], s.A[5], s.A[7], rev64(s.A[0]), rev64(s.A[2]), rev64(s.A[4]), rev64(s.A[6])};
-#endif
-}
-// For a ray R leaving the move in decreasing bit order (normal orientation)
-// and the run set A: the squares of R & A above R's highest square not in A
-// (x = R & ~A, nonzero whenever R & A is)
-__device__ __forceinline__ u64 run_prefix_dec(u64 R, u64 A) {
-    const u64 x = andn(R, A);
-    const u32 hi = (u32)(x >> 32), lo = (u32)x;
-    const u32 top = hi ? 63u - (u32)__builtin_clz(hi) : 31u - (u32)__builtin_clz(lo | 1u);
-    const u64 below = dec64(2ull << top);  // bits 0..top (2 << 63 wraps to 0: all)
-    return bitop3<0x20>(R, below, A);       // R & ~below & A
 }
 
 // The flips of the move at square sq (bit mv) in two parts, both including
@@ -325,13 +302,8 @@ __device__ __forceinline__ Flips flips_col(u64 mv, const RunSets& r, const u64* 
     u64 fr = bitop3<0xBA>(r.rA0, lshl1_add(rmv, r.rA0), rmv);  // west, in reversed space
     f = or3(f, run_prefix(col[0 * 64], r.A3), run_prefix(col[1 * 64], r.A5));
     f = or2(f, run_prefix(col[2 * 64], r.A7));
-#if OTH_FLIPS_NORMAL_DEC
-    f = or3(f, run_prefix_dec(col[3 * 64], r.rA2), run_prefix_dec(col[4 * 64], r.rA4));
-    f = or2(f, run_prefix_dec(col[5 * 64], r.rA6));
-#else
     fr = or3(fr, run_prefix(col[3 * 64], r.rA2), run_prefix(col[4 * 64], r.rA4));
     fr = or2(fr, run_prefix(col[5 * 64], r.rA6));
-#endif
     return Flips{f, rev64(fr)};
 }
 __device__ __forceinline__ Flips flips_rays(u32 sq, const RunSets& r, const u64* tab) {
@@ -425,34 +397,11 @@ __device__ __forceinline__ u64 flips_carry(u32 sq, u64 P, u64 O) {
 }
 
 // legal moves only (no run sets kept) — for child positions / next-state masks
-template <int ORDER = OTH_FILL_ORDER>
+template <int ORDER = kFillOrder>
 __device__ __forceinline__ u64 moves(u64 P, u64 O) {
     Position s;
     analyse<ORDER>(P, O, s);
     return s.legal;
-}
-
-// Legal moves only, the reach folded in direction by direction (round 5, A/B
-// for the 1-ply policies' child evaluation: analyse keeps all eight run sets
-// live until the reach; here each direction's run set dies at its shift).
-// Same result as moves().
-__device__ __forceinline__ u64 moves_lean(u64 P, u64 O) {
-    const u64 Oi = and2(O, INNER_FILES);
-    u64 m = sh<1, true>(east_run(P, Oi));
-    m = or2(m, sh<1, false>(rev64(east_run(rev64(P), rev64(Oi)))));
-    {
-        const PairProp v = pair_prop<8>(O);
-        m = or3(m, sh<8, true>(and2(ks<8, true>(P, v), O)), sh<8, false>(and2(ks<8, false>(P, v), O)));
-    }
-    {
-        const PairProp d = pair_prop<9>(Oi);
-        m = or3(m, sh<9, true>(and2(ks<9, true>(P, d), O)), sh<9, false>(and2(ks<9, false>(P, d), O)));
-    }
-    {
-        const PairProp d = pair_prop<7>(Oi);
-        m = or3(m, sh<7, true>(and2(ks<7, true>(P, d), O)), sh<7, false>(and2(ks<7, false>(P, d), O)));
-    }
-    return bitop3<0x04>(P, m, O);  // ~P & m & ~O
 }
 
 // Board.puttables(Empty) (board.py:46-52 with piece = Empty, hostile(Empty) =
@@ -490,10 +439,6 @@ __device__ __forceinline__ u32 add_lshl3(u32 a, u32 b) {
 // level's offset, and the three level offsets are disjoint bits (32 | 16 | 8):
 // one v_or3 and one v_add_lshl with the table entry give the offset
 // (31 -> 24 VALU per pick with the address arithmetic).
-#ifndef OTH_PICK_CNDMASK
-#define OTH_PICK_CNDMASK 1
-#endif
-#if OTH_PICK_CNDMASK
 // One bisection level in VOP3 with the borrow as the select: b = (k < c) from
 // v_sub_co_u32's borrow, k = b ? k : k - c and off = b ? 0 : S by two
 // v_cndmask_b32_e64, where min(k, k - c) cost a v_min_u32 (a slow
@@ -536,24 +481,6 @@ __device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t
     const u32 lvl = (u32)__builtin_amdgcn_bitop3_b32(b32, s16, s8, 0xFE);
     return add_lshl3(lvl, tab[byte * 8u + k]);
 }
-#else
-__device__ __forceinline__ u32 kth_bit_off(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
-    const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    const bool up = k >= c_lo;
-    u32 w = up ? hi : lo;
-    const u32 b32 = up ? 32u : 0u;
-    k = min(k, k - c_lo);
-    u32 c = __popc(w & 0xFFFFu);
-    const u32 s16 = k >= c ? 16u : 0u;
-    k = min(k, k - c);
-    w >>= s16;
-    c = __popc(w & 0xFFu);
-    const u32 s8 = k >= c ? 8u : 0u;
-    k = min(k, k - c);
-    const u32 byte = __builtin_amdgcn_ubfe(w, s8, 8);
-    return add_lshl3(b32 | s16 | s8, tab[byte * 8u + k]);
-}
-#endif
 __device__ __forceinline__ u32 kth_bit_tab(u64 x, u32 k, u32 c_lo, const uint8_t* tab) {
     return kth_bit_off(x, k, c_lo, tab) >> 3;
 }

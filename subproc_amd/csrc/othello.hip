@@ -101,17 +101,8 @@ __device__ __forceinline__ void eval_weights_to_lds(const EvalWeights& ew, int* 
 // The products by 24-bit multiplies (v_mul_i32_i24, full rate) where a plain
 // int multiply is v_mul_lo_u32, a multi-pass instruction: the weights are
 // int8 and the counts <= 64, so every product and partial sum is exact in
-// 24 bits.  OTH_EVAL_MUL24=0: A/B builds only.
-#ifndef OTH_EVAL_MUL24
-#define OTH_EVAL_MUL24 1
-#endif
-__device__ __forceinline__ int eval_mul(int w, int c) {
-#if OTH_EVAL_MUL24
-    return __mul24(w, c);
-#else
-    return w * c;
-#endif
-}
+// 24 bits.
+__device__ __forceinline__ int eval_mul(int w, int c) { return __mul24(w, c); }
 __device__ __forceinline__ int eval_linear(const int* w, u64 mine, u64 mob) {
     int v = eval_mul(w[0], (int)__popcll(mob));
 #pragma unroll
@@ -138,17 +129,10 @@ __device__ __forceinline__ const int* child_row(u64 P, u64 O, const int* w_tab) 
     if (POLICY != OTH_POLICY_EVAL) return w_tab;
     return w_tab + kEvalRow * eval_shard((u32)__popcll(P | O) + 1u);
 }
-#ifndef OTH_CHILD_LEAN  // A/B builds: the greedy child's mobility by moves_lean (bitboard.hpp)
-#define OTH_CHILD_LEAN 0
-#endif
 template <int POLICY>
 __device__ __forceinline__ u32 child_key(u64 P, u64 O, const RunSets& s, u32 sq, const u64* rays, const int* row) {
     place(P, O, flips_rays(sq, s, rays));
-#if OTH_CHILD_LEAN
-    if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves_lean(O, P)) << 6) | sq;
-#else
     if (POLICY == OTH_POLICY_GREEDY) return ((u32)__popcll(moves(O, P)) << 6) | sq;
-#endif
     int w[OTH_EVAL_FEATURES];
 #pragma unroll
     for (int j = 0; j < OTH_EVAL_FEATURES; j++) w[j] = row[j];
@@ -192,16 +176,9 @@ __device__ __forceinline__ u32 lane_choose(const Position& pos, u64 P, u64 O, co
 // list, one entry per loop iteration of the busiest lane, ~13 VALU each; the
 // chunks need no list.)  cap == 0 (OTH_COOP_CAP=0, tests) takes lane_choose
 // for every choosing lane instead.
-#ifndef OTH_COOP_HOLD_EVAL  // round 5: the eval kernel holds its parent record too (A/B: 0 rereads it)
-#define OTH_COOP_HOLD_EVAL 1
-#endif
-// OTH_COOP_FORCED=1 (A/B builds only): a mover with exactly one legal move plays
-// it without scoring its child (same games: no RNG is drawn either way).  It
-// cut greedy VALU by 0.9% but ran 1.3% (greedy) / 5% (eval) slower per launch
-// (round 5, tools/diag/forced_ab.sh, profiles/r05_notes.md)
-#ifndef OTH_COOP_FORCED
-#define OTH_COOP_FORCED 0
-#endif
+// (Round 5 A/B, not shipped: a mover with exactly one legal move playing it
+// without scoring its child cut greedy VALU by 0.9% but ran 1.3% (greedy) /
+// 5% (eval) slower per launch; tools/diag/r05_variants.patch.)
 struct CoopWave {
     u64 rec[64][10];  // parent lane: P, O, its RunSets (8 words; A1's bit 0, a1, carries the eval table)
     u64 legal[64];    // parent lane's legal mask (0: not choosing)
@@ -274,7 +251,6 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
     // mostly evaluated their own children (PMC: same VALU per child within
     // 2%, round 5, profiles/r05_notes.md); held, eval runs at round 3's speed
     // (3.810 against 3.817 ms per 1M-game launch, 3.945 rereading)
-    constexpr bool kHold = POLICY != OTH_POLICY_EVAL || OTH_COOP_HOLD_EVAL;
     u64 m = 0, Pp = 0, Op = 0;
     RunSets ps = {};
     const int* row = w_s;
@@ -284,16 +260,15 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
     };
     if (cnt_mine) {
         m = cw.legal[p];
-        if (kHold) enter(p);
+        enter(p);
         if (k0) m &= ~0ull << kth_bit_tab(m, k0, (u32)__popc((u32)m), kth_tab);  // skip the chunk's predecessors
     }
     for (u32 r = 0; r < cnt_mine; r++) {
         if (m == 0) {  // the next parent with moves (one exists, above p < 63: t0 + r < T)
             p = (u32)__ffsll((unsigned long long)(with_moves & (~0ull << (p + 1)))) - 1u;
             m = cw.legal[p];
-            if (kHold) enter(p);
+            enter(p);
         }
-        if (!kHold) enter(p);
         const u32 sq = (u32)__builtin_ctzll(m);  // m != 0 here: no zero case (__ffsll's select)
         m &= m - 1;
         atomicMin(&cw.best[p], child_key<POLICY>(Pp, Op, ps, sq, rays, row));
@@ -440,10 +415,7 @@ __device__ __forceinline__ void step_board(int64_t i, ulonglong2 b, u32 t, u32 m
     if (nturn && r >= 0) nturn[i] = (uint8_t)(nturn[i] + 1);
 }
 
-#ifndef OTH_STEP_PER_THREAD
-#define OTH_STEP_PER_THREAD 1
-#endif
-constexpr int kStepPerThread = OTH_STEP_PER_THREAD;
+constexpr int kStepPerThread = 1;
 // kStepPerThread boards per thread, kBlock * gridDim apart (each load
 // instruction still coalesced), all loaded before any is computed
 __global__ __launch_bounds__(kBlock) void step_kernel(const u64* boards_in, const uint8_t* turn_in,
@@ -564,21 +536,20 @@ struct RolloutArgs {
     u32 n_rand_a, n_rand_b;
     int swap;
     uint8_t* a_black;
-    // OTH_HANDOFF builds (A/B): a fresh random batch hands its games over to the
-    // wave's LDS pool once no more than handoff_k lanes are still playing
+    // the random policy's batch-tail hand-over (on by default; OTH_HANDOFF_K=0
+    // in the environment turns it off): a fresh batch hands its games over to
+    // the wave's LDS pool once no more than handoff_k lanes are still playing
     u32 handoff_k;
 };
 
-// Batch-tail compaction (A/B builds only, OTH_HANDOFF=1; round 3's variant on
-// the round-4 kernel, the round-4 verdict's item 5).  When at most handoff_k
+// Batch-tail compaction (shipped since round 5 in the random-policy kernel
+// without move records; OTH_HANDOFF_K=0 in the environment turns it off at
+// run time, tools/diag/handoff.patch removes it).  When at most handoff_k
 // lanes of a fresh batch are still playing (a __ballot of the loop's live
 // lanes, __popcll), the wave parks those games -- the whole lane state, 32 B
 // -- in its LDS pool, compacted to the pool's top by mbcnt, and dequeues the
 // next batch; once 64 games are parked they are played out as a batch of their
 // own, and a wave that finds the queue empty plays out what it has parked.
-#ifndef OTH_HANDOFF
-#define OTH_HANDOFF 1
-#endif
 constexpr u32 kHandoffK = 16;                       // the default K (env OTH_HANDOFF_K)
 constexpr u32 kHandoffKMax = 16;                    // the pool's capacity allows K up to this
 constexpr int kPoolCap = 64 + (int)kHandoffKMax;    // < 64 parked + at most K more per batch
@@ -590,12 +561,6 @@ struct Parked {
 };
 static_assert(sizeof(Parked) == 32, "two 16-B LDS accesses per parked game");
 constexpr u64 kParkedGame = ~0ull;
-
-#ifdef OTH_DIAG
-// per wave: start, end (s_memrealtime), hw_id, and (random policy) the wave's
-// issued plies (executions of the ply step) << 32 | its lanes' plies
-__device__ unsigned long long* g_diag;
-#endif
 
 // Move records of the random policy (RECORD): a lane's record is one 128-byte
 // row and the batch's 64 games are consecutive, so the wave's records are one
@@ -617,32 +582,18 @@ constexpr size_t rec_stage_bytes(int policy, bool record) {
 
 // the random loop's fill order (bitboard.hpp analyse): with the VOP3 logic,
 // 7-8-9 leaves the fewest same-bank v_bitop3_b32 in its loop (tools/valu_mix.py)
-#ifndef OTH_RANDOM_FILL_ORDER
-#define OTH_RANDOM_FILL_ORDER 789
-#endif
-constexpr int kRandomFillOrder = OTH_RANDOM_FILL_ORDER;
+constexpr int kRandomFillOrder = 789;
+// every rollout kernel: >= 4 waves/SIMD, <= 128 VGPRs (greedy at 5, 96 VGPRs,
+// ran slower: profiles/r05_notes.md)
+constexpr int kRolloutWavesPerSimd = 4;
 template <int POLICY, bool RECORD, bool RUNNER = false>
-#ifndef OTH_EVAL_WAVES_PER_SIMD  // A/B builds: the eval kernels' occupancy floor (launch bounds)
-#define OTH_EVAL_WAVES_PER_SIMD 4
-#endif
-#ifndef OTH_GREEDY_WAVES_PER_SIMD  // A/B builds: the greedy kernels' occupancy floor
-#define OTH_GREEDY_WAVES_PER_SIMD 4
-#endif
-__global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WAVES_PER_SIMD
-                                     : POLICY == OTH_POLICY_GREEDY ? OTH_GREEDY_WAVES_PER_SIMD
-                                                                   : 4) void rollout_kernel(
-    RolloutArgs a) {  // >= 4 waves/SIMD: <= 128 VGPRs
-#ifdef OTH_DIAG
-    const unsigned long long diag_t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long diag_iters = 0, diag_wave_iters = 0;
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-#endif
+__global__ __launch_bounds__(kBlock, kRolloutWavesPerSimd) void rollout_kernel(RolloutArgs a) {
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
     __shared__ u64 rays[kTabRows * 64];
     __shared__ int w_s[POLICY == OTH_POLICY_EVAL ? 2 * kEvalTable : 1];
     __shared__ CoopWave coop[POLICY == OTH_POLICY_RANDOM ? 1 : kBlock / 64];
-    constexpr bool kPool = OTH_HANDOFF && POLICY == OTH_POLICY_RANDOM && !RECORD && !RUNNER;
+    constexpr bool kPool = POLICY == OTH_POLICY_RANDOM && !RECORD && !RUNNER;
     __shared__ Parked pool_s[kPool ? kBlock / 64 : 1][kPool ? kPoolCap : 1];
     for (int k = threadIdx.x; k < OTH_HIST_BINS; k += kBlock) hist_s[k] = 0;
     kth_table_init(kth_tab);
@@ -762,10 +713,6 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
             // discs: inside it, the block ran whenever any lane of the wave
             // ended, ~7 times per batch.
             auto ply_of = [&](u64& X, u64& Y) -> bool {
-#ifdef OTH_DIAG
-                diag_iters++;  // this lane's plies
-                if ((u32)lane == (u32)__builtin_amdgcn_readfirstlane(lane)) diag_wave_iters++;  // the wave's
-#endif
                 Position pos;
                 analyse<kRandomFillOrder>(X, Y, pos);
                 const u64 legal = pos.legal;
@@ -844,9 +791,6 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
                 if (a.a_black) a.a_black[g] = (uint8_t)ab;
             }
             while (__ballot(active)) {
-#ifdef OTH_DIAG
-                diag_iters++;
-#endif
                 bool moving = false, choose = false;
                 u32 sq = 0;
                 Position pos;
@@ -893,14 +837,11 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
                                 sq = pick_legal(legal, rng, kth_tab);
                                 if (side == OTH_BLACK) rem_b--;
                                 else rem_w--;
-                            } else if (OTH_COOP_FORCED && !(legal & (legal - 1))) {
-                                sq = (u32)__builtin_ctzll(legal);  // one legal move: no children to score
                             } else {
                                 choose = true;
                             }
                         } else if ((int)ply >= a.n_random) {
-                            if (OTH_COOP_FORCED && !(legal & (legal - 1))) sq = (u32)__builtin_ctzll(legal);
-                            else choose = true;  // decided below, by the whole wave
+                            choose = true;  // decided below, by the whole wave
                         } else {
                             sq = pick_legal(legal, rng, kth_tab);
                         }
@@ -937,23 +878,6 @@ __global__ __launch_bounds__(kBlock, POLICY == OTH_POLICY_EVAL     ? OTH_EVAL_WA
         }
     }
 
-#ifdef OTH_DIAG
-    for (int off = 32; off >= 1; off >>= 1) {
-        diag_iters += __shfl_xor(diag_iters, off);
-        diag_wave_iters += __shfl_xor(diag_wave_iters, off);
-    }
-    if (lane == 0 && g_diag) {
-        unsigned hwid;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* d = g_diag + 4 * wave;
-        d[0] = diag_t0;
-        d[1] = __builtin_amdgcn_s_memrealtime();
-        d[2] = ((unsigned long long)xcc << 32) | hwid;
-        d[3] = (diag_wave_iters << 32) | (diag_iters & 0xffffffffull);
-    }
-#endif
     // plies: wave reduction, one LDS atomic per wave
     for (int off = 32; off >= 1; off >>= 1) plies_sum += __shfl_xor(plies_sum, off);
     if (lane == 0) atomicAdd(&hist_s[132], (unsigned long long)plies_sum);
@@ -1546,60 +1470,20 @@ __device__ __forceinline__ u64 td_skey_of(ulonglong2 b, u32 sd) {
     return td_skey::encode((u32)__popcll(b.x | b.y), (u32)__popcll(mob), r);
 }
 
-// one thread per recorded position (g, p); rows of an oth_replay table
-// (row_off == nullptr: row g*OTH_POS_STRIDE + p) or of an oth_replay_rows one
-// (row row_off[g] + p)
-__global__ __launch_bounds__(kBlock) void td_updates_kernel(const u64* __restrict__ pos,
-                                                            const int64_t* __restrict__ row_off,
-                                                            const uint8_t* __restrict__ plies,
-                                                            const int64_t* __restrict__ base,
-                                                            const double* __restrict__ lam_pow,
-                                                            int64_t* __restrict__ keys, double* __restrict__ vals,
-                                                            u64* __restrict__ words, int64_t n) {
-    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (idx >= n * OTH_POS_STRIDE) return;
-    const int64_t g = idx / OTH_POS_STRIDE;
-    const u32 p = (u32)(idx - g * OTH_POS_STRIDE);
-    const u32 np = min<u32>(plies[g], OTH_MOVES_STRIDE);
-    if (p > np) return;
-    const ulonglong2* row = reinterpret_cast<const ulonglong2*>(pos) + (row_off ? row_off[g] : g * OTH_POS_STRIDE);
-    const ulonglong2 term = row[np];
-    const int vb = __popcll(term.x) - __popcll(term.y);  // value_for_black (41); white gets -vb (42)
-    const ulonglong2 b = row[p];
-    const int64_t j = base[g] + 2 * (int64_t)(np - p);
-    if (words) {  // oth_td_updates_packed: (key, value_side, turn_left) in one word
-        const u64 tl = np - p;
-        const u64 t = tl << OTH_TD_PACK_TURN_SHIFT;
-        words[j] = ((u64)(vb + 64) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_BLACK);
-        words[j + 1] = ((u64)(64 - vb) << OTH_TD_PACK_VALUE_SHIFT) | t | td_skey_of(b, OTH_WHITE);
-        return;
-    }
-    const double lam = lam_pow[np - p];
-    keys[j] = td_key(b, OTH_BLACK);
-    vals[j] = (double)vb * lam;
-    keys[j + 1] = td_key(b, OTH_WHITE);
-    vals[j + 1] = (double)(-vb) * lam;
-}
-
 // The same updates, one wave per game (round 5): lane p takes the game's
 // positions p, p + 64, ... .  One thread per (g, p) slot of the 129-row stride
 // leaves about half the lanes of the waves that do work idle (a game records
 // ~62 positions of its 129 slots, and the waves straddle games); here a wave
 // idles only on the lanes past the game's own positions.  The game's plies,
 // row offset, base and terminal row are wave-uniform (scalar loads).  A wave
-// takes OTH_TD_UPD_GAMES = 4 games (late round 5): 195 -> 177 us per 32.2M
+// takes kTdUpdGames = 4 games (late round 5): 195 -> 177 us per 32.2M
 // updates (1: 195, 2: 179-183, 8: 175-177 at 112 VGPRs; tools/diag/td_ab.sh).
-// OTH_TD_UPD_WAVE=0 builds the per-slot kernel for these entry points (A/B).
-#ifndef OTH_TD_UPD_WAVE
-#define OTH_TD_UPD_WAVE 1
-#endif
-// OTH_TD_UPD_GAMES games per wave, one after the other: their scalar loads
+// (The round-4 kernel, one thread per (g, p) slot: tools/diag/r05_variants.patch.)
+// kTdUpdGames games per wave, one after the other: their scalar loads
 // (plies, row offset, base, terminal row) and first-round row loads are issued
 // before any game's words are computed, so a wave waits on one dependent
 // chain of loads for all of them instead of one chain per game.
-#ifndef OTH_TD_UPD_GAMES
-#define OTH_TD_UPD_GAMES 4
-#endif
+constexpr int kTdUpdGames = 4;
 // the words (or key/value pairs) of position p of a game whose terminal
 // position np gives value_for_black vb; first update index jb
 template <bool WORDS>
@@ -1627,7 +1511,7 @@ __global__ __launch_bounds__(kBlock) void td_updates_wave_kernel(const u64* __re
                                                                  const double* __restrict__ lam_pow,
                                                                  int64_t* __restrict__ keys, double* __restrict__ vals,
                                                                  u64* __restrict__ words, int64_t n) {
-    constexpr int G = OTH_TD_UPD_GAMES;
+    constexpr int G = kTdUpdGames;
     const int64_t g0 =
         ((int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) * G;
     if (g0 >= n) return;
@@ -1758,9 +1642,7 @@ __device__ __forceinline__ double td_range(double v, const double* __restrict__ 
 // SHORT: every segment here is shorter than 3 chunks (long_min <= 3 * kTdChunk),
 // so the kernel has no ring of loads and needs a fraction of the registers:
 // more waves in flight for the millions of 1- to 3-update keys.
-#ifndef OTH_TD_EMA_PRE  // A/B builds
-#define OTH_TD_EMA_PRE 8
-#endif
+constexpr int kTdEmaPre = 8;
 template <bool SHORT>
 __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict__ vals,
                                                         const int64_t* __restrict__ seg_off,
@@ -1773,10 +1655,10 @@ __global__ __launch_bounds__(kBlock) void td_ema_kernel(const double* __restrict
     if (long_min > 0 && e - i >= long_min) return;
     double v = init ? init[s] : 0.0;
     if (SHORT) {
-        // the first OTH_TD_EMA_PRE values loaded together (predicated), so
+        // the first kTdEmaPre values loaded together (predicated), so
         // most keys (1 to a few updates) wait on one round trip for them
         // rather than one per update; the rest one by one
-        constexpr int kPre = OTH_TD_EMA_PRE;
+        constexpr int kPre = kTdEmaPre;
         double x[kPre > 0 ? kPre : 1];
 #pragma unroll
         for (int k = 0; k < kPre; k++) x[k] = i + k < e ? vals[i + k] : 0.0;
@@ -1847,10 +1729,7 @@ constexpr int64_t kSpecMaxLen = 1ll << 27;  // longer keys (beyond any batch in 
 // keys of >= 3 warm-ups are split (at a = 0.03: 5,826 updates, the single-lane
 // chain's longest as in round 3; at 4 warm-ups of the longer round-4 warm-up,
 // 7,768, the long-key kernel took 199 us against 130)
-#ifndef OTH_SPEC_MIN_WARMS  // A/B builds
-#define OTH_SPEC_MIN_WARMS 3
-#endif
-constexpr int64_t kSpecMinWarms = OTH_SPEC_MIN_WARMS;
+constexpr int64_t kSpecMinWarms = 3;
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
@@ -1936,10 +1815,7 @@ __global__ __launch_bounds__(kBlock) void td_spec_select_kernel(const int64_t* _
 // it sequentially, so no part is ever written out of bounds.
 // one block of kPlanThreads: beside the short keys' kernel (the EMA's side
 // streams) a block of 1,024 threads waited 40-67 us for a CU with room for it
-#ifndef OTH_TD_PLAN_THREADS  // A/B builds
-#define OTH_TD_PLAN_THREADS 256
-#endif
-constexpr int kPlanThreads = OTH_TD_PLAN_THREADS, kPlanWaves = kPlanThreads / 64;
+constexpr int kPlanThreads = 256, kPlanWaves = kPlanThreads / 64;
 __global__ __launch_bounds__(kPlanThreads) void td_spec_plan_kernel(int64_t* __restrict__ hdr,
                                                                     SpecPlanEntry* __restrict__ plan, int64_t cap) {
     __shared__ u32 wsum[2][kPlanWaves];
@@ -2091,10 +1967,7 @@ inline size_t spec_scratch_bytes(int64_t n_long, int64_t n_values) {
 // from LDS while the next stage is in flight, so the time is the chain's.
 // (round 5: 1,024 before; at 33 KiB of LDS per one-wave block only 4 keys'
 // chains ran per CU: 131 -> 92 us per batch at 512, 106-110 at 256)
-#ifndef OTH_TD_STAGE  // A/B builds
-#define OTH_TD_STAGE 512
-#endif
-constexpr int kTdStage = OTH_TD_STAGE;         // doubles per LDS stage
+constexpr int kTdStage = 512;         // doubles per LDS stage
 constexpr int kTdStageLoads = kTdStage / 64;   // loads per lane per stage
 // (ystage rows padded by one chunk: the chain prefetches the next chunk's y
 // unconditionally)
@@ -2300,16 +2173,12 @@ DeviceState* device_state() {
 }
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int launched() { return status(hipGetLastError()); }
-// the TD update stream (td_updates_wave_kernel / td_updates_kernel)
+// the TD update stream (td_updates_wave_kernel)
 static int td_updates_launch(const u64* pos, const int64_t* row_off, const uint8_t* plies, const int64_t* base,
                              const double* lam_pow, int64_t* keys, double* vals, u64* words, int64_t n, hipStream_t s) {
-    if (OTH_TD_UPD_WAVE)
-        (words ? td_updates_wave_kernel<true> : td_updates_wave_kernel<false>)<<<
-            blocks_for((n + OTH_TD_UPD_GAMES - 1) / OTH_TD_UPD_GAMES * 64), kBlock, 0, s>>>(
-            pos, row_off, plies, base, lam_pow, keys, vals, words, n);
-    else
-        td_updates_kernel<<<blocks_for(n * OTH_POS_STRIDE), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys,
-                                                                             vals, words, n);
+    (words ? td_updates_wave_kernel<true> : td_updates_wave_kernel<false>)<<<
+        blocks_for((n + kTdUpdGames - 1) / kTdUpdGames * 64), kBlock, 0, s>>>(pos, row_off, plies, base, lam_pow, keys,
+                                                                               vals, words, n);
     return launched();
 }
 
@@ -2403,8 +2272,8 @@ int rollout_launch(const uint64_t* start, const uint8_t* start_turn, uint64_t se
     // (lane_choose), so the per-lane path runs from ordinary positions
     a.coop_cap = env_int("OTH_COOP_CAP", 1) == 0 ? 0u : 1u;
     a.last_ticket = 64ull * ((u64)((n + 63) / 64) + (u64)grid * (kBlock / 64) - 1ull);
-    // (OTH_HANDOFF builds: game indices are parked as 32 bits)
-    a.handoff_k = OTH_HANDOFF && n <= 0xFFFFFFFFll
+    // (game indices are parked as 32 bits)
+    a.handoff_k = n <= 0xFFFFFFFFll
                       ? (u32)std::min(std::max(env_int("OTH_HANDOFF_K", (int)kHandoffK), 0), (int)kHandoffKMax)
                       : 0u;
     hipStream_t st = (hipStream_t)stream;

@@ -28,30 +28,30 @@
 #include "../../include/othello.h"
 #include "td_skey.hpp"
 
-// a packed word's turn_left as an index into lam_pow (OTH_POS_STRIDE
-// entries): clamped, so a word that did not come from oth_td_updates_packed
-// (turn_left above 128) cannot read past the table
+// packed words seen with a turn_left beyond lam_pow's OTH_POS_STRIDE entries
+// (not words oth_td_updates_packed wrote: a corrupt or foreign word array),
+// counted by every reader since the last oth_td_word_errors reset
+__device__ unsigned long long g_td_bad_words;
+// a turn_left field as an index into lam_pow: clamped, so such a word never
+// reads past the table, and counted, so it is reported instead of hidden
+__device__ __forceinline__ uint32_t td_turn_clamp(uint32_t t) {
+    if (t < (uint32_t)OTH_POS_STRIDE) return t;
+    atomicAdd(&g_td_bad_words, 1ull);
+    return (uint32_t)OTH_POS_STRIDE - 1u;
+}
 __device__ __forceinline__ uint32_t td_turn_idx(uint64_t w) {
-    return min((uint32_t)(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK, (uint32_t)OTH_POS_STRIDE - 1u);
+    return td_turn_clamp((uint32_t)(w >> OTH_TD_PACK_TURN_SHIFT) & OTH_TD_PACK_TURN_MASK);
 }
 
 namespace {
 
-// onesweep digit width, items per thread and block size (build knobs for A/B
-// builds only, profiles/r05_notes.md; the product build uses the defaults)
-#ifndef OTH_SORT_BITS
-#define OTH_SORT_BITS 9
-#endif
-#ifndef OTH_SORT_IPT
-#define OTH_SORT_IPT 8
-#endif
-#ifndef OTH_SORT_BLOCK
-#define OTH_SORT_BLOCK 1024
-#endif
+// onesweep digit width, items per thread and block size (tuned, round 5:
+// profiles/r05_notes.md)
+constexpr unsigned kSortBits = 9, kSortIpt = 8, kSortBlock = 1024;
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<OTH_SORT_BLOCK, OTH_SORT_IPT>,
-                                        rocprim::kernel_config<OTH_SORT_BLOCK, OTH_SORT_IPT>, OTH_SORT_BITS,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<kSortBlock, kSortIpt>,
+                                        rocprim::kernel_config<kSortBlock, kSortIpt>, kSortBits,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
 // packed words -> (key, value): the value recomputed from the payload exactly
@@ -68,593 +68,16 @@ __global__ __launch_bounds__(256) void td_unpack_kernel(const uint64_t* __restri
     values[i] = (double)vs * lam_pow[td_turn_idx(w)];
 }
 
-// ---------------------------------------------------------------------------
-// The grouping sort (oth_td_sort_packed / oth_td_sort_unpack): a stable LSD
-// radix sort of 64-bit words by their low `bits` bits, written for gfx950 in
-// the onesweep form -- one read and one write of the words per digit:
-//   * sort_hist_kernel: one read of the input, the histograms of every
-//     digit position at once (LDS counters per block, then global atomics);
-//   * sort_pass_kernel, once per digit: a block takes the next tile of
-//     kSortTile words (an atomic ticket, so tiles start in order), ranks
-//     them stably in LDS, publishes its per-digit counts and looks back over
-//     the tiles before it for their running totals (decoupled look-back, one
-//     flag word per tile polled 64 tiles at a time; below),
-//     then writes the tile out digit by digit through an LDS stage, so
-//     consecutive lanes store consecutive words of one digit's run.
-//     (n < 2^32: the counts are 32-bit.)
-// Ranking: a wave ranks its 64 words of a round by ballots over the digit's
-// bits (the lanes with the same digit: `peers`), the lane's place among them
-// by mbcnt, and the wave's running count of the digit in LDS, read by every
-// lane and bumped by the lowest lane of each peer group (one wave's LDS
-// instructions execute in order, so each round sees the last one's counts).
-// Words keep their order: within a wave by round then lane, across the
-// block's waves by the waves' prefix counts, across tiles by the look-back.
-// The last pass can write the unpacked (key, value) pairs straight away
-// (oth_td_sort_unpack: oth_td_unpack fused in).
-#ifndef OTH_SORT_ROCPRIM  // 1: rocPRIM's onesweep (the shipped build while the own sort trails it)
-#define OTH_SORT_ROCPRIM 1
-#endif
-#ifndef OTH_SORT_DIGIT
-#define OTH_SORT_DIGIT 9
-#endif
-// tiles of 8 waves x 32 rounds = 16,384 words (round 5 A/B over 4,096-16,384:
-// fewer, larger tiles shorten the look-back chains; profiles/r05_notes.md)
-#ifndef OTH_SORT_WAVES
-#define OTH_SORT_WAVES 8
-#endif
-#ifndef OTH_SORT_ROUNDS
-#define OTH_SORT_ROUNDS 32
-#endif
-#ifndef OTH_SORT_GROUP
-#define OTH_SORT_GROUP 16
-#endif
-constexpr int kSortGroup = OTH_SORT_GROUP;  // tiles per look-back group
-// a look-back poll that has not seen its word after this many polls gives up
-// (and sets a bit of the sort's error word) rather than hang the GPU
-constexpr uint32_t kSortSpinMax = 1u << 18;
-// diagnostic builds only (wrong output, for timing the parts): no look-back;
-// the tile written back in place, unscattered
-// the look-back of the own sort: 1 = the plain per-digit walk (faster at
-// 16,384-word tiles: 1.002 against 1.038 ms), 0 = hints and group sums
-#ifndef OTH_SORT_LOOK_SIMPLE
-#define OTH_SORT_LOOK_SIMPLE 1
-#endif
-#ifndef OTH_SORT_DIAG_NOLOOK
-#define OTH_SORT_DIAG_NOLOOK 0
-#endif
-#ifndef OTH_SORT_DIAG_LINEAR
-#define OTH_SORT_DIAG_LINEAR 0
-#endif
-#ifndef OTH_SORT_DIAG_TIME
-#define OTH_SORT_DIAG_TIME 0
-#endif
-constexpr int kSortDigitBits = OTH_SORT_DIGIT;
-constexpr int kSortDigits = 1 << kSortDigitBits;
-constexpr int kSortWaves = OTH_SORT_WAVES;
-constexpr int kSortRounds = OTH_SORT_ROUNDS;
-constexpr int kSortThreads = 64 * kSortWaves;
-constexpr int kSortTile = kSortThreads * kSortRounds;
-constexpr int kSortMaxPasses = (64 + kSortDigitBits - 1) / kSortDigitBits;
-constexpr int kSortHistBlock = 256;
-static_assert(kSortDigits % kSortThreads == 0, "digits per thread");
-constexpr int kSortDigitsPerThread = kSortDigits / kSortThreads;
-
-// the digit of pass q: bits [q * D, min((q + 1) * D, bits)) -- the last
-// pass's digit is narrower when D does not divide `bits` (the bits above are
-// the packed word's payload, which must not order anything)
-__device__ __forceinline__ uint32_t sort_digit(uint64_t w, int shift, uint32_t mask) {
-    return (uint32_t)(w >> shift) & mask;
-}
-__host__ __device__ __forceinline__ uint32_t sort_mask(int bits, int q) {
-    const int w = bits - q * kSortDigitBits;
-    return w >= kSortDigitBits ? (uint32_t)(kSortDigits - 1) : (1u << w) - 1u;
-}
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-// inclusive scan of x over the wave's 64 lanes (DPP row shifts and row broadcasts)
-__device__ __forceinline__ uint32_t sort_wave_scan(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return x;
-}
-
-// the histograms of every digit position: hist[p * kSortDigits + d] (zeroed
-// by the launcher)
-// (kSortHistCopies copies of the counters, lanes spread over them: a wave's
-// lanes with the same digit -- the disc field of the opening plies, say --
-// serialise on one LDS address otherwise; dynamic LDS, copies x passes x
-// digits words).  Each thread reads two words per 16-byte load, four loads in
-// flight.
-#ifndef OTH_SORT_HIST_COPIES
-#define OTH_SORT_HIST_COPIES 4
-#endif
-constexpr int kSortHistCopies = OTH_SORT_HIST_COPIES;
-__global__ __launch_bounds__(kSortHistBlock) void sort_hist_kernel(const uint64_t* __restrict__ in, int64_t n,
-                                                                   int passes, int bits,
-                                                                   unsigned long long* __restrict__ hist) {
-    extern __shared__ uint32_t hdyn[];
-    const int per = passes * kSortDigits;
-    for (int e = threadIdx.x; e < kSortHistCopies * per; e += kSortHistBlock) hdyn[e] = 0;
-    __syncthreads();
-    uint32_t* hc = hdyn + (threadIdx.x & (kSortHistCopies - 1)) * per;
-    auto count = [&](uint64_t w) {
-        for (int p = 0; p < passes; p++)
-            atomicAdd(&hc[p * kSortDigits + sort_digit(w, p * kSortDigitBits, sort_mask(bits, p))], 1u);
-    };
-    // a word before the first 16-byte boundary (a caller's offset pointer)
-    // alone, then pairs, then a last odd word
-    const int lead = (reinterpret_cast<uintptr_t>(in) & 15) ? 1 : 0;
-    if (lead && n > 0 && blockIdx.x == 0 && threadIdx.x == 0) count(in[0]);
-    const int64_t n2 = (n - lead) >> 1;  // word pairs
-    const ulonglong2* in2 = reinterpret_cast<const ulonglong2*>(in + lead);
-    const int64_t stride = (int64_t)gridDim.x * kSortHistBlock;
-    int64_t i = (int64_t)blockIdx.x * kSortHistBlock + threadIdx.x;
-    for (; i + 3 * stride < n2; i += 4 * stride) {
-        ulonglong2 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = in2[i + u * stride];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            count(v[u].x);
-            count(v[u].y);
-        }
-    }
-    for (; i < n2; i += stride) {
-        const ulonglong2 v = in2[i];
-        count(v.x);
-        count(v.y);
-    }
-    if (((n - lead) & 1) && blockIdx.x == 0 && threadIdx.x == 0) count(in[n - 1]);
-    __syncthreads();
-    for (int e = threadIdx.x; e < per; e += kSortHistBlock) {
-        uint32_t c = 0;
-        for (int k = 0; k < kSortHistCopies; k++) c += hdyn[k * per + e];
-        if (c) atomicAdd(&hist[e], (unsigned long long)c);
-    }
-}
-
-// One digit pass (see above).  UNPACK: write keys_out / vals_out (the word's
-// low OTH_TD_KEY_BITS, and value_side * lam_pow[turn_left]) instead of out.
-template <bool UNPACK>
-__global__ __launch_bounds__(kSortThreads) void sort_pass_kernel(
-    const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int64_t n, int shift, uint32_t dmask, uint32_t tag,
-    const unsigned long long* __restrict__ hist, unsigned* __restrict__ status, size_t vec_off, size_t gsum_off,
-    int64_t ngroups, unsigned* __restrict__ ticket, unsigned* __restrict__ err, size_t diag_off, const double* __restrict__ lam_pow, int64_t* __restrict__ keys_out,
-    double* __restrict__ vals_out) {
-    __shared__ uint64_t stage[kSortTile];
-    __shared__ uint32_t wcnt[kSortWaves][kSortDigits];  // a wave's running counts, then its prefix over waves
-    __shared__ uint32_t blk_off[kSortDigits];           // the tile's digits: exclusive prefix of their counts
-    __shared__ long long gbase[kSortDigits];            // output index of the tile's slot 0, per digit
-    __shared__ uint32_t wsum[kSortWaves];
-    __shared__ unsigned long long hsum[kSortWaves];
-    __shared__ uint32_t tile_s, look_k, look_inc;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (tid == 0) tile_s = atomicAdd(ticket, 1u);
-    for (int e = tid; e < kSortWaves * kSortDigits; e += kSortThreads) (&wcnt[0][0])[e] = 0;
-    __syncthreads();
-    const int64_t tile = tile_s;
-#if OTH_SORT_DIAG_TIME
-    // (diagnostic builds: s_memtime at entry, before the look-back, after it,
-    // at exit; the scratch's diag area, 4 words per tile per pass)
-    unsigned long long* const dgt =
-        reinterpret_cast<unsigned long long*>(status + diag_off) + ((size_t)(tag - 1) * gridDim.x + tile) * 4;
-    const unsigned long long dt0 = __builtin_amdgcn_s_memtime();
-#endif
-    const int64_t t0 = tile * kSortTile, wbase = t0 + (int64_t)wave * (kSortRounds * 64);
-    // the wave's words, every round's load in flight before the first is ranked
-    uint64_t v[kSortRounds];
-#pragma unroll
-    for (int k = 0; k < kSortRounds; k++) {
-        const int64_t i = wbase + k * 64 + lane;
-        v[k] = i < n ? in[i] : 0ull;
-    }
-    // (the counters read and bumped by wavefront-scope atomics on the LDS
-    // array itself: a volatile pointer to them made hipcc use FLAT accesses
-    // with a vmcnt wait each)
-    uint32_t rank[kSortRounds];
-#pragma unroll
-    for (int k = 0; k < kSortRounds; k++) {
-        const bool valid = wbase + k * 64 + lane < n;
-        const uint32_t d = sort_digit(v[k], shift, dmask);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < kSortDigitBits; b++) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        const uint32_t below = lanes_below(peers);
-        const uint32_t old =
-            valid ? __hip_atomic_load(&wcnt[wave][d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0u;
-        if (valid && below == 0)
-            __hip_atomic_store(&wcnt[wave][d], old + (uint32_t)__popcll(peers), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-        rank[k] = old + below;
-    }
-    __syncthreads();
-    // per digit: the waves' exclusive prefix (in place) and the tile's count;
-    // the global offset of the digit (exclusive scan of this pass's histogram)
-    uint32_t tot[kSortDigitsPerThread];
-    unsigned long long hcnt[kSortDigitsPerThread];
-    uint32_t tsum = 0;
-    unsigned long long hs = 0;
-#pragma unroll
-    for (int j = 0; j < kSortDigitsPerThread; j++) {
-        const int d = tid * kSortDigitsPerThread + j;
-        uint32_t s = 0;
-#pragma unroll
-        for (int w = 0; w < kSortWaves; w++) {
-            const uint32_t c = wcnt[w][d];
-            wcnt[w][d] = s;
-            s += c;
-        }
-        tot[j] = s;
-        tsum += s;
-        hcnt[j] = hist[d];
-        hs += hcnt[j];
-    }
-    // exclusive scans over the digits (thread-major: thread t owns digits
-    // t*DPT .. t*DPT+DPT-1): the tile's counts and the pass histogram
-    const uint32_t ti = sort_wave_scan(tsum);
-    unsigned long long hi = hs;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(hi, o);
-        if (lane >= o) hi += y;
-    }
-    if (lane == 63) {
-        wsum[wave] = ti;
-        hsum[wave] = hi;
-    }
-    __syncthreads();
-    uint32_t tpre = ti - tsum;
-    unsigned long long hpre = hi - hs;
-    for (int w = 0; w < wave; w++) {
-        tpre += wsum[w];
-        hpre += hsum[w];
-    }
-    // publish the tile's counts, look back over the tiles before it, publish
-    // the inclusive counts.
-    // * One 64-bit word per (tile, digit): flag (1 = the tile's own count,
-    //   2 = inclusive of every tile before it) << 62 | pass tag << 56 | count,
-    //   self-validating, so no fence orders anything (a reader takes a word
-    //   only once its tag is this pass's and its flag is set; on gfx950 a
-    //   release fence per tile would write back the XCD's whole L2, the
-    //   sort's scattered output included: 3-5 ms per sort, measured).
-    // * One hint word per tile (tag << 2 | the same flag), stored after the
-    //   tile's words: wave 0 polls the hints of up to 64 tiles at once.
-    // * Group sums: the tiles of a group of kSortGroup add their counts into
-    //   the group's sum (returning atomics, so the adds are done before the
-    //   group's done-counter is bumped).  A block sums tile by tile only within
-    //   its own group; before it, a whole group at a time (one vector), back to
-    //   the nearest group whose last tile is inclusive.  The first wave of
-    //   blocks of a pass starts before any tile is inclusive: tile by tile,
-    //   the last of them would each read hundreds of tiles' counts (1.2 GB of
-    //   status reads per pass, measured 2.34 ms per sort against 0.89 without
-    //   any look-back).
-    {  // the tile's digit offsets first: the LDS staging below needs no look-back
-        uint32_t tp = tpre;
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++) {
-            blk_off[tid * kSortDigitsPerThread + j] = tp;
-            tp += tot[j];
-        }
-    }
-    uint32_t* hint = status;
-    uint64_t* word = reinterpret_cast<uint64_t*>(status + vec_off);
-    uint32_t* gsum = status + gsum_off;  // this pass's group sums (groups x digits), then done counters
-    uint32_t* gdone = gsum + (size_t)ngroups * kSortDigits;
-    uint64_t* mine = word + (size_t)tile * kSortDigits;
-    const uint64_t tagw = (uint64_t)tag << 56;
-    const int64_t grp = tile / kSortGroup, first_in_grp = grp * kSortGroup;
-#pragma unroll
-    for (int j = 0; j < kSortDigitsPerThread; j++)
-        __hip_atomic_store(mine + tid * kSortDigitsPerThread + j, ((tile ? 1ull : 2ull) << 62) | tagw | tot[j],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (tid == 0)
-        __hip_atomic_store(hint + tile, (tag << 2) | (tile ? 1u : 2u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!OTH_SORT_LOOK_SIMPLE) {  // (the group sums: unused by the plain look-back)
-        uint32_t dep = 0;
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++)
-            if (tot[j])
-                dep |= __hip_atomic_fetch_add(gsum + (size_t)grp * kSortDigits + tid * kSortDigitsPerThread + j, tot[j],
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::"v"(dep) : "memory");  // every add of this thread done
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(gdone + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // the tile in digit order in LDS, while the tiles before it publish
-#pragma unroll
-    for (int k = 0; k < kSortRounds; k++) {
-        if (wbase + k * 64 + lane < n) {
-            const uint32_t d = sort_digit(v[k], shift, dmask);
-            stage[blk_off[d] + wcnt[wave][d] + rank[k]] = v[k];
-        }
-    }
-    unsigned long long acc[kSortDigitsPerThread];
-    bool open[kSortDigitsPerThread];
-#pragma unroll
-    for (int j = 0; j < kSortDigitsPerThread; j++) {
-        acc[j] = 0;
-        open[j] = tile > 0 && !OTH_SORT_DIAG_NOLOOK;
-    }
-    // a tile's words: summed (own or inclusive); need_inc: poll until inclusive
-    auto take_tile = [&](int64_t t, bool need_inc) {
-        const uint64_t* tw = word + (size_t)t * kSortDigits + tid * kSortDigitsPerThread;
-        uint64_t x[kSortDigitsPerThread];
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++)
-            x[j] = open[j] ? __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++) {
-            if (!open[j]) continue;
-            // (a hint may be visible before the words it follows: poll them)
-            for (uint32_t spin = 0;
-                 ((x[j] >> 56) & 63u) != tag || (x[j] >> 62) == 0 || (need_inc && (x[j] >> 62) != 2); spin++) {
-                if (spin > kSortSpinMax) {  // never expected: report, do not hang the GPU
-                    atomicOr(err, 1u);
-                    break;
-                }
-                x[j] = __hip_atomic_load(tw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            acc[j] += x[j] & ((1ull << 56) - 1);
-            if ((x[j] >> 62) == 2) open[j] = false;
-        }
-    };
-#if OTH_SORT_DIAG_TIME
-    const unsigned long long dt1 = __builtin_amdgcn_s_memtime();
-#endif
-#if OTH_SORT_LOOK_SIMPLE
-    // (A/B) the plain decoupled look-back: each thread walks its digits'
-    // words back tile by tile, no block barrier, until an inclusive one
-#pragma unroll
-    for (int j = 0; j < kSortDigitsPerThread; j++) {
-        const uint64_t* dw = word + tid * kSortDigitsPerThread + j;
-        for (int64_t t = tile - 1; open[j] && t >= 0; t--) {
-            uint64_t x = __hip_atomic_load(dw + (size_t)t * kSortDigits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t spin = 0; ((x >> 56) & 63u) != tag || (x >> 62) == 0; spin++) {
-                if (spin > kSortSpinMax) {
-                    atomicOr(err, 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                x = __hip_atomic_load(dw + (size_t)t * kSortDigits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            acc[j] += x & ((1ull << 56) - 1);
-            if ((x >> 62) == 2) open[j] = false;
-        }
-    }
-    int64_t hi_t = -1;
-    bool done = true;
-#else
-    // phase A: the tiles of this block's group before it, up to 64 hints a poll
-    int64_t hi_t = tile - 1;
-    bool done = tile == 0 || OTH_SORT_DIAG_NOLOOK;
-#endif
-    while (!done && hi_t >= first_in_grp) {
-        if (wave == 0) {
-            uint32_t k = 0;
-            for (uint32_t spin = 0;; spin++) {
-                if (spin > kSortSpinMax) {
-                    if (lane == 0) atomicOr(err, 2u);
-                    k = (uint32_t)(hi_t - first_in_grp + 1);
-                    break;
-                }
-                const int64_t t = hi_t - lane;
-                const uint32_t f =
-                    t >= first_in_grp ? __hip_atomic_load(hint + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                const bool ready = (f >> 2) == tag && (f & 3u) != 0;
-                const uint64_t mr = __ballot(ready), mi = __ballot(ready && (f & 3u) == 2u);
-                const uint32_t first_gap = mr == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mr);
-                const uint32_t near_inc = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
-                if (near_inc < first_gap) {  // own counts, then an inclusive tile
-                    k = near_inc + 1;
-                    break;
-                }
-                if (first_gap > 0 && (first_gap < 64u || hi_t - 63 < first_in_grp)) {
-                    k = first_gap;  // own counts (to the group's first tile, or a tile not yet published)
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);  // the nearest tile has not published yet
-            }
-            if (lane == 0) look_k = k;
-        }
-        __syncthreads();
-        const int64_t k = look_k;
-        for (int64_t i = 0; i < k; i++) take_tile(hi_t - i, false);
-        hi_t -= k;
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++) any |= open[j];
-        done = !__syncthreads_or(any);  // every digit reached an inclusive count
-    }
-    // phase B: whole groups before this block's, up to 64 a poll: complete
-    // group sums back to the nearest group whose last tile is inclusive
-    int64_t hi_g = grp - 1;
-    while (!done) {
-        if (wave == 0) {
-            uint32_t k = 0, inc = 0;
-            for (uint32_t spin = 0;; spin++) {
-                if (spin > kSortSpinMax || hi_g < 0) {
-                    if (lane == 0) atomicOr(err, hi_g < 0 ? 8u : 4u);
-                    k = (uint32_t)max<int64_t>(hi_g + 1, 0);
-                    inc = 0;
-                    break;
-                }
-                const int64_t g = hi_g - lane;
-                uint32_t fd = 0, fh = 0;
-                if (g >= 0) {
-                    fd = __hip_atomic_load(gdone + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    fh = __hip_atomic_load(hint + (g + 1) * kSortGroup - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const uint64_t mr = __ballot(g >= 0 && fd == (uint32_t)kSortGroup);
-                const uint64_t mi = __ballot(g >= 0 && fh == ((tag << 2) | 2u));
-                const uint32_t first_gap = mr == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mr);
-                const uint32_t near_inc = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
-                if (near_inc <= first_gap && near_inc < 64u) {  // complete groups, then an inclusive tile
-                    k = near_inc;
-                    inc = 1;
-                    break;
-                }
-                if (first_gap > 0) {  // complete groups only: sum them, look further back
-                    k = first_gap;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (lane == 0) {
-                look_k = k;
-                look_inc = inc;
-            }
-        }
-        __syncthreads();
-        const int64_t k = look_k;
-        const bool inc = look_inc;
-        for (int64_t i = 0; i < k; i++) {
-            const uint32_t* gv = gsum + (size_t)(hi_g - i) * kSortDigits + tid * kSortDigitsPerThread;
-#pragma unroll
-            for (int j = 0; j < kSortDigitsPerThread; j++)
-                if (open[j]) acc[j] += __hip_atomic_load(gv + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        hi_g -= k;
-        if (hi_g < 0) done = true;  // (only after a reported error)
-        if (inc) {
-            take_tile((hi_g + 1) * kSortGroup - 1, true);  // the inclusive last tile of group hi_g
-            done = true;
-        }
-        __syncthreads();  // look_k / look_inc read before wave 0 writes them again
-    }
-    if (tile) {
-#pragma unroll
-        for (int j = 0; j < kSortDigitsPerThread; j++)
-            __hip_atomic_store(mine + tid * kSortDigitsPerThread + j, (2ull << 62) | tagw | (acc[j] + tot[j]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(hint + tile, (tag << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int j = 0; j < kSortDigitsPerThread; j++) {
-        const int d = tid * kSortDigitsPerThread + j;
-        gbase[d] = (long long)(hpre + acc[j]) - (long long)tpre;
-        tpre += tot[j];
-        hpre += hcnt[j];
-    }
-    __syncthreads();
-#if OTH_SORT_DIAG_TIME
-    const unsigned long long dt2 = __builtin_amdgcn_s_memtime();
-#endif
-    const int nv = (int)min<int64_t>(kSortTile, n - t0);
-#pragma unroll 4
-    for (int s = tid; s < nv; s += kSortThreads) {
-        const uint64_t w = stage[s];
-        const int64_t pos = OTH_SORT_DIAG_LINEAR ? t0 + s : gbase[sort_digit(w, shift, dmask)] + s;
-        if (UNPACK) {
-            const int vs = (int)(w >> OTH_TD_PACK_VALUE_SHIFT) - 64;
-            keys_out[pos] = td_skey::to_key(w & ((1ull << OTH_TD_SKEY_BITS) - 1));
-            vals_out[pos] = (double)vs * lam_pow[td_turn_idx(w)];
-        } else {
-            out[pos] = w;
-        }
-    }
-#if OTH_SORT_DIAG_TIME
-    __syncthreads();
-    if (tid == 0) {
-        dgt[0] = dt0;
-        dgt[1] = dt1;
-        dgt[2] = dt2;
-        dgt[3] = __builtin_amdgcn_s_memtime();
-    }
-#endif
-}
-
-// scratch: [ping-pong words (n) | histograms | tickets | status (tiles x digits)]
-struct SortPlan {
-    int passes;
-    int64_t tiles;
-    int64_t groups;
-    size_t words_off, hist_off, ticket_off, status_off, vec_off, gsum_off, diag_off, bytes;
-};
-inline SortPlan sort_plan(int64_t n, int bits) {
-    SortPlan p;
-    p.passes = (bits + kSortDigitBits - 1) / kSortDigitBits;
-    p.tiles = (n + kSortTile - 1) / kSortTile;
-    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
-    p.words_off = 0;
-    p.hist_off = al((size_t)n * sizeof(uint64_t));
-    p.ticket_off = al(p.hist_off + (size_t)p.passes * kSortDigits * sizeof(unsigned long long));
-    p.status_off = al(p.ticket_off + (size_t)(kSortMaxPasses + 1) * sizeof(unsigned));  // tickets, error word
-    // status: the tiles' hint words, then their (tile, digit) words (vec_off:
-    // in 32-bit units, even)
-    const size_t tiles = (size_t)std::max<int64_t>(p.tiles, 1);
-    p.vec_off = (tiles + 63) / 64 * 64;
-    // then per pass the group sums and the groups' done counters (32-bit units)
-    p.groups = (int64_t)((tiles + kSortGroup - 1) / kSortGroup);
-    p.gsum_off = p.vec_off + tiles * 2 * kSortDigits;
-    // (diagnostic builds: then 4 timestamps per tile per pass, 64-bit aligned)
-    p.diag_off = (p.gsum_off + (size_t)p.passes * ((size_t)p.groups * (kSortDigits + 1) + 64) + 1) / 2 * 2;
-    p.bytes = al(p.status_off + p.diag_off * sizeof(uint32_t) +
-                 (OTH_SORT_DIAG_TIME ? (size_t)p.passes * tiles * 4 * sizeof(uint64_t) : 0));
-    return p;
-}
-// the sort of n words by bits [0, bits): into out (keys NULL) or unpacked into
-// keys / vals; temp of sort_plan(n, bits).bytes
-hipError_t sort_words(const uint64_t* in, uint64_t* out, int64_t n, int bits, const double* lam_pow, int64_t* keys,
-                      double* vals, void* temp, hipStream_t st) {
-    const SortPlan p = sort_plan(n, bits);
-    char* t = static_cast<char*>(temp);
-    uint64_t* tmp = reinterpret_cast<uint64_t*>(t + p.words_off);
-    unsigned long long* hist = reinterpret_cast<unsigned long long*>(t + p.hist_off);
-    unsigned* ticket = reinterpret_cast<unsigned*>(t + p.ticket_off);
-    unsigned* status = reinterpret_cast<unsigned*>(t + p.status_off);
-    // histograms, tickets and every status word start at 0 (one fill per
-    // sort: the pass tags tell this sort's passes apart, the fill any earlier
-    // use of the scratch)
-    hipError_t e = hipMemsetAsync(t + p.hist_off, 0, p.bytes - p.hist_off, st);
-    if (e != hipSuccess) return e;
-    sort_hist_kernel<<<512, kSortHistBlock, kSortHistCopies * p.passes * kSortDigits * sizeof(uint32_t), st>>>(
-        in, n, p.passes, bits, hist);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // the passes ping-pong so that the last one writes the output: words into
-    // `out` and tmp; unpacked, the words through tmp and the keys array
-    uint64_t* bufA = keys ? reinterpret_cast<uint64_t*>(keys) : out;
-    uint64_t* bufB = tmp;
-    const uint64_t* src = in;
-    for (int q = 0; q < p.passes; q++) {
-        const bool last = q == p.passes - 1;
-        // the destination of pass q: the buffers alternate so that the last
-        // pass lands in `out` (or the unpacked arrays)
-        uint64_t* dst = ((p.passes - 1 - q) & 1) ? bufB : bufA;
-        if (keys && last) dst = nullptr;
-        if (keys && last)
-            sort_pass_kernel<true><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
-                src, nullptr, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
-                p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
-                ticket + kSortMaxPasses, p.diag_off, lam_pow, keys, vals);
-        else
-            sort_pass_kernel<false><<<(unsigned)p.tiles, kSortThreads, 0, st>>>(
-                src, dst, n, q * kSortDigitBits, sort_mask(bits, q), (uint32_t)(q + 1), hist + (size_t)q * kSortDigits, status,
-                p.vec_off, p.gsum_off + (size_t)q * ((size_t)p.groups * (kSortDigits + 1) + 64), p.groups, ticket + q,
-                ticket + kSortMaxPasses, p.diag_off, nullptr, nullptr, nullptr);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        src = dst;
-    }
-    return hipSuccess;
-}
+// The grouping sort (oth_td_sort_packed / oth_td_sort_unpack) is rocPRIM's
+// onesweep radix sort (SortConfig above): the one vendor kernel on a §8 path.
+// Round 5 built and A/B'd an own onesweep for gfx950 (ballot ranking, LDS
+// stage, decoupled look-back): correct but 1.00-1.04 ms per 32.2M words
+// against rocPRIM's 0.82, and 0.80 even with the look-back removed (wrong
+// output, timing only), so it was not shipped; round 6 removed it from the
+// source (tools/diag/td_own_sort.patch restores it; profiles/r05_notes.md).
 
 constexpr int kMergeBlock = 256;
-#ifndef OTH_MERGE_K  // A/B builds only
-#define OTH_MERGE_K 8
-#endif
-#ifndef OTH_MERGE_DEFER  // A/B builds only
-#define OTH_MERGE_DEFER 1
-#endif
-constexpr int kMergeK = OTH_MERGE_K;                     // merged positions per thread
+constexpr int kMergeK = 8;                               // merged positions per thread
 constexpr int kMergeTile = kMergeBlock * kMergeK;        // per block
 constexpr int kLookupK = 8;
 constexpr int kLookupTile = kMergeBlock * kLookupK;
@@ -780,7 +203,6 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
     double ov[kMergeK];
     uint64_t os[kMergeK];
     unsigned long long smin = ~0ull, smax = 0;
-#if OTH_MERGE_DEFER
     // the merge walk first, recording each output's batch index; then the
     // new_before loads of all of them at once (in the walk they were one
     // dependent global load per step; round 4)
@@ -824,38 +246,6 @@ __global__ __launch_bounds__(kMergeBlock) void td_merge_kernel(const int64_t* __
             smax = max(smax, (unsigned long long)os[q] + 1);
         }
     }
-#else
-#pragma unroll
-    for (int q = 0; q < kMergeK; q++) {
-        os[q] = ~0ull;  // no output
-        const int m = t0 + q;
-        if (m >= t1) continue;
-        const int64_t gm = d0 + m;
-        if (i < na && (j >= nb || sk[i] < sk[na + j])) {
-            const int64_t key = sk[i];
-            if (key != prev_b) {  // not the table copy of the batch key just taken
-                const int64_t bc = b0 + j;
-                os[q] = (uint64_t)(gm - (bc - new_before[bc]));
-                ok[q] = key;
-                ov[q] = sv[i];
-            }
-            i++;
-        } else {
-            const int64_t bj = b0 + j;
-            const int64_t key = sk[na + j];
-            os[q] = (uint64_t)(gm - (bj - new_before[bj]));
-            ok[q] = key;
-            ov[q] = sv[na + j];
-            prev_b = key;
-            j++;
-        }
-        if (os[q] >= n_out) os[q] = ~0ull;
-        if (os[q] != ~0ull) {
-            smin = min(smin, (unsigned long long)os[q]);
-            smax = max(smax, (unsigned long long)os[q] + 1);
-        }
-    }
-#endif
     if (smin != ~0ull) {
         atomicMin(&range[0], smin);
         atomicMax(&range[1], smax);
@@ -1056,10 +446,7 @@ hipError_t merge_splits(const int64_t* A, int64_t nA, const int64_t* B, int64_t 
 // rounds of 64 words per wave: 8 (late round 5; tools/diag/td_ab.sh, two
 // passes, count / write pass per 32.2M words: 4 rounds 78 / 137 us, 6: 75 /
 // 134, 8: 71 / 133, 16: 79 / 137, 32: 103 / 153)
-#ifndef OTH_SEG_ROUNDS  // A/B builds
-#define OTH_SEG_ROUNDS 8
-#endif
-constexpr int kSegRounds = OTH_SEG_ROUNDS;
+constexpr int kSegRounds = 8;
 constexpr int kSegWaveKeys = 64 * kSegRounds;
 constexpr int kSegBlock = 256;
 constexpr int kSegWavesPerBlock = kSegBlock / 64;
@@ -1112,7 +499,7 @@ __global__ __launch_bounds__(kSegBlock) void td_seg_kernel(const int64_t* __rest
         const int64_t i = base + r * 64 + lane;
         if (WORDS && WRITE && i < n) {
             const int vs = (int)(payload[r] >> (OTH_TD_PACK_VALUE_SHIFT - OTH_TD_PACK_TURN_SHIFT)) - 64;
-            values[i] = (double)vs * lam_pow[min(payload[r] & OTH_TD_PACK_TURN_MASK, (uint32_t)OTH_POS_STRIDE - 1u)];
+            values[i] = (double)vs * lam_pow[td_turn_clamp(payload[r] & OTH_TD_PACK_TURN_MASK)];
         }
         int64_t before = __shfl_up(k[r], 1);
         if (lane == 0) before = prev_last;
@@ -1297,7 +684,7 @@ int oth_td_merge(const int64_t* old_keys, const double* old_vals, int64_t n_old,
 int oth_td_merge_after_lookup(const int64_t* old_keys, const double* old_vals, int64_t n_old, const int64_t* upd_keys,
                               const double* upd_vals, const int64_t* new_before, int64_t n_upd, int64_t* out_keys,
                               double* out_vals, const void* lookup_temp, void* stream) {
-    if (kMergeTile != kLookupTile) return OTH_EINVAL;  // (an A/B build's OTH_MERGE_K)
+    static_assert(kMergeTile == kLookupTile, "the lookup's splits serve the merge");
     if (n_old < 0 || n_upd < 0 || (n_old > 0 && (!old_keys || !old_vals)) ||
         (n_upd > 0 && (!upd_keys || !upd_vals || !new_before || !lookup_temp)) ||
         (n_old + n_upd > 0 && (!out_keys || !out_vals)))
@@ -1309,7 +696,6 @@ int oth_td_merge_after_lookup(const int64_t* old_keys, const double* old_vals, i
 int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n, void* temp, size_t* temp_bytes,
                        void* stream) {
     if (n < 0 || !temp_bytes) return OTH_EINVAL;
-#if OTH_SORT_ROCPRIM
     if (!temp) {  // size query: no work, no launch
         size_t bytes = 0;
         const hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, bytes, words_in, words_out, (size_t)n,
@@ -1323,26 +709,11 @@ int oth_td_sort_packed(const uint64_t* words_in, uint64_t* words_out, int64_t n,
     const hipError_t e = rocprim::radix_sort_keys<SortConfig>(temp, bytes, words_in, words_out, (size_t)n,
                                                               0, OTH_TD_SKEY_BITS, (hipStream_t)stream);
     return e == hipSuccess ? OTH_OK : -(int)e;
-#else
-    const size_t need = sort_plan(n, OTH_TD_SKEY_BITS).bytes;
-    if (!temp) {  // size query: no work, no launch
-        *temp_bytes = need;
-        return OTH_OK;
-    }
-    if (n > 0 && (!words_in || !words_out || words_in == words_out)) return OTH_EINVAL;
-    if (n >= (1ll << 32)) return OTH_EINVAL;  // 32-bit counts
-    if (*temp_bytes < need) return OTH_EINVAL;
-    if (n == 0) return OTH_OK;
-    const hipError_t e = sort_words(words_in, words_out, n, OTH_TD_SKEY_BITS, nullptr, nullptr, nullptr, temp,
-                                    (hipStream_t)stream);
-    return e == hipSuccess ? OTH_OK : -(int)e;
-#endif
 }
 
 int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t* keys, double* values, int64_t n,
                        void* temp, size_t* temp_bytes, void* stream) {
     if (n < 0 || !temp_bytes) return OTH_EINVAL;
-#if OTH_SORT_ROCPRIM
     // rocPRIM's sort of the words into the scratch, then the unpack kernel
     size_t sort_bytes = 0;
     hipError_t e = rocprim::radix_sort_keys<SortConfig>(nullptr, sort_bytes, words_in, (uint64_t*)nullptr, (size_t)n,
@@ -1350,9 +721,6 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
     if (e != hipSuccess) return -(int)e;
     sort_bytes = (sort_bytes + 255) / 256 * 256;
     const size_t need = sort_bytes + (size_t)std::max<int64_t>(n, 1) * sizeof(uint64_t);
-#else
-    const size_t need = sort_plan(n, OTH_TD_SKEY_BITS).bytes;
-#endif
     if (!temp) {  // size query: no work, no launch
         *temp_bytes = need;
         return OTH_OK;
@@ -1363,17 +731,12 @@ int oth_td_sort_unpack(const uint64_t* words_in, const double* lam_pow, int64_t*
     if (n >= (1ll << 32)) return OTH_EINVAL;  // 32-bit counts
     if (*temp_bytes < need) return OTH_EINVAL;
     if (n == 0) return OTH_OK;
-#if OTH_SORT_ROCPRIM
     uint64_t* sorted = reinterpret_cast<uint64_t*>(static_cast<char*>(temp) + sort_bytes);
     e = rocprim::radix_sort_keys<SortConfig>(temp, sort_bytes, words_in, sorted, (size_t)n, 0, OTH_TD_SKEY_BITS,
                                              (hipStream_t)stream);
     if (e != hipSuccess) return -(int)e;
     td_unpack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(sorted, lam_pow, keys, values, n);
     e = hipGetLastError();
-#else
-    const hipError_t e = sort_words(words_in, nullptr, n, OTH_TD_SKEY_BITS, lam_pow, keys, values, temp,
-                                    (hipStream_t)stream);
-#endif
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 
@@ -1453,6 +816,17 @@ int oth_td_new_before(const uint8_t* is_new, int64_t n, int64_t* new_before, voi
     e = hipGetLastError();
     if (e == hipSuccess)
         e = hipMemcpyAsync(new_before + n, counts, sizeof(int64_t), hipMemcpyDeviceToDevice, st);
+    return e == hipSuccess ? OTH_OK : -(int)e;
+}
+
+int oth_td_word_errors(uint64_t* count, int reset, void* stream) {
+    if (!count) return OTH_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    void* dev = nullptr;
+    hipError_t e = hipGetSymbolAddress(&dev, HIP_SYMBOL(g_td_bad_words));
+    if (e == hipSuccess) e = hipMemcpyAsync(count, dev, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && reset) e = hipMemsetAsync(dev, 0, sizeof(uint64_t), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
     return e == hipSuccess ? OTH_OK : -(int)e;
 }
 

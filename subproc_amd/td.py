@@ -164,6 +164,20 @@ def _with_scratch(fn, args, stream, device, what):
     return temp
 
 
+def word_errors(device="cuda", reset=True):
+    """The number of packed update words with a turn_left past the lam_pow
+    table that the TD readers (unpack, sort_unpack, segments_words) met on
+    `device` since the last reset (include/othello.h oth_td_word_errors): 0
+    unless a word array was corrupted or did not come from
+    oth_td_updates_packed.  Synchronizes the current stream."""
+    d = torch.device(device)
+    with torch.cuda.device(d):
+        out = ctypes.c_uint64(0)
+        check(_lib.load().oth_td_word_errors(ctypes.byref(out), int(bool(reset)),
+                                              torch.cuda.current_stream(d).cuda_stream), "oth_td_word_errors")
+    return int(out.value)
+
+
 class StateMap:
     """Device-resident 'param:state:*' table: sorted int64 keys + float64 values."""
 

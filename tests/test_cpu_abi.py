@@ -234,5 +234,10 @@ def test_td_unpack_clamps_turn_left_host_build():
     tl = np.array([0, 128, 129, 0xFFFFF], np.uint64)
     w = np.ascontiguousarray((np.uint64(64 + 3) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)))
     keys, vals = np.zeros(4, np.int64), np.zeros(4, np.float64)
+    cnt = ctypes.c_uint64(0)
+    assert lib().oth_td_word_errors(ctypes.byref(cnt), 1, None) == 0
     assert lib().oth_td_unpack(P(w), P(lam), P(keys), P(vals), 4, None) == 0
     np.testing.assert_array_equal(vals, 3.0 * lam[[0, 128, 128, 128]])
+    # the two words past the table are counted (oth_td_word_errors), not only clamped
+    assert lib().oth_td_word_errors(ctypes.byref(cnt), 1, None) == 0 and cnt.value == 2
+    assert lib().oth_td_word_errors(ctypes.byref(cnt), 0, None) == 0 and cnt.value == 0

@@ -572,23 +572,63 @@ def test_td_segments_pair(long_min):
         np.testing.assert_array_equal(np.sort(li.d.cpu().numpy()[:nl]), want)
 
 
+def word_errors(reset=False):
+    """oth_td_word_errors on both builds: (device count, host count)."""
+    gpu, cpu = _lib.load(), oracle.cpu_abi()
+    g, c = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    assert gpu.oth_td_word_errors(ctypes.byref(g), int(reset), torch.cuda.current_stream().cuda_stream) == 0
+    assert cpu.oth_td_word_errors(ctypes.byref(c), int(reset), None) == 0
+    return int(g.value), int(c.value)
+
+
 def test_td_unpack_clamps_turn_left_pair():
     """Words whose turn_left exceeds 128 (not from oth_td_updates_packed):
-    both builds read lam_pow[128], in oth_td_unpack and in
-    oth_td_segments_words, never past the table."""
+    both builds read lam_pow[128], in oth_td_unpack, oth_td_segments_words and
+    oth_td_sort_unpack, never past the table, and count every such word read
+    (oth_td_word_errors) instead of hiding it."""
+    word_errors(reset=True)
     lam = Buf(np.array([0.9 ** j for j in range(129)], np.float64))
     tl = np.array([0, 128, 129, 0xFFFFF] * 16, np.uint64)
     w = Buf((np.uint64(64 - 5) << np.uint64(56)) | (tl << np.uint64(_lib.TD_PACK_TURN_SHIFT)))
     n = len(tl)
+    bad = int((tl > 128).sum())
     keys, vals = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64))
     both("oth_td_unpack", w, lam, keys, vals, n)
     same(keys, vals)
     np.testing.assert_array_equal(vals.h, -5.0 * lam.h[np.minimum(tl, 128).astype(np.int64)])
+    assert word_errors() == (bad, bad)
     off, uk, li, cnt, val = (Buf(np.zeros(n + 1, np.int64)), Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.int64)),
                              Buf(np.zeros(2, np.int64)), Buf(np.zeros(n, np.float64)))
     both_scratch("oth_td_segments_words", w, lam, n, 48, off, uk, li, cnt, val)
     same(cnt, val)
     np.testing.assert_array_equal(val.h, vals.h)
+    assert word_errors() == (2 * bad, 2 * bad)
+    ko, vo = Buf(np.zeros(n, np.int64)), Buf(np.zeros(n, np.float64))
+    both_scratch("oth_td_sort_unpack", w, lam, ko, vo, n)
+    same(ko, vo)
+    assert word_errors(reset=True) == (3 * bad, 3 * bad)
+    assert word_errors() == (0, 0)
+
+
+def test_td_word_errors_zero_on_the_learner_path():
+    """A StateMap update over real GPU books (oth_td_updates_packed words through
+    the sort, the segments and the EMA) reads no out-of-range word; a corrupted
+    copy of its words is reported."""
+    from subproc_amd import ops
+    from subproc_amd.td import StateMap, lam_pow_table, word_errors as td_word_errors
+
+    td_word_errors(reset=True)
+    r = ops.rollout(4096, 0x5EED, 0, "random", record_moves=True, device=DEV)
+    sm = StateMap(DEV)
+    sm.update_rows(ops.replay_rows(r.moves, r.plies), r.plies)
+    assert len(sm) > 0 and td_word_errors() == 0
+    w = torch.randint(0, 1 << 36, (1000,), dtype=torch.int64, device=DEV)
+    w[::10] |= 300 << _lib.TD_PACK_TURN_SHIFT  # 100 words with turn_left 300
+    lam = torch.tensor(lam_pow_table(), dtype=torch.float64, device=DEV)
+    k, v = torch.empty_like(w), torch.empty(1000, dtype=torch.float64, device=DEV)
+    _lib.check(_lib.load().oth_td_unpack(w.data_ptr(), lam.data_ptr(), k.data_ptr(), v.data_ptr(), 1000,
+                                         torch.cuda.current_stream().cuda_stream), "oth_td_unpack")
+    assert td_word_errors() == 100 and td_word_errors() == 0
 
 
 def test_td_segments_words_pair():

@@ -340,7 +340,13 @@ def _bench_rollout(torch, dist, dev, stream, args, policy, world, rank, use_dist
 
     n = args.games
     hists = torch.zeros((args.warmup + args.steps, HIST_BINS), dtype=torch.int64, device=dev)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
+    # side streams from the process's one pool (ops._side_streams, which
+    # rollout_batches uses too): every bench line reuses the same few streams
+    # instead of creating its own, so the HIP runtime's hardware queues
+    # (GPU_MAX_HW_QUEUES, 4 per process) are not spread over ever more streams
+    from subproc_amd.ops import _side_streams
+
+    streams = [stream] + _side_streams(dev, nstreams - 1)
     bufs = [(torch.empty((n, 2), dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int8, device=dev),
              torch.empty(n, dtype=torch.uint8, device=dev)) for _ in streams]
     # one work word per stream (include/othello.h: 0 before and after each launch)

@@ -214,13 +214,9 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, const uint8_t* kth_tab, u32 lane, u32 cap) {
-    if (cap == 0) return need ? lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0)) : 64u;
-    const u64 legal = need ? pos.legal : 0ull;
-    const u32 cnt = (u32)__popcll(legal);
-    const u32 incl = wave_incl_scan(cnt);
-    const u32 T = (u32)__builtin_amdgcn_readlane((int)incl, 63);
-    const u32 R = (T + 63u) >> 6;
-    cw.legal[lane] = legal;
+    // the record is published first, on either path: the caller plays the
+    // chosen move from it (its run sets need not stay in VGPRs across the
+    // children, round 6)
     if (need) {
         u64* r = cw.rec[lane];
         r[0] = P;
@@ -228,8 +224,15 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
         RunSets rs = run_sets(pos);  // reversed once per parent, not per child
         if (POLICY == OTH_POLICY_EVAL) rs.A1 |= (u64)(tbl & 1u);
         *reinterpret_cast<RunSets*>(r + 2) = rs;
-        cw.best[lane] = 0xFFFFFFFFu;
     }
+    if (cap == 0) return need ? lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0)) : 64u;
+    const u64 legal = need ? pos.legal : 0ull;
+    const u32 cnt = (u32)__popcll(legal);
+    const u32 incl = wave_incl_scan(cnt);
+    const u32 T = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    const u32 R = (T + 63u) >> 6;
+    cw.legal[lane] = legal;
+    if (need) cw.best[lane] = 0xFFFFFFFFu;
     // this lane's chunk of the children: [t0, t0 + cnt_mine).  Its first
     // parent, the last lane whose first child is <= t0, by a binary search of
     // the exclusive scan, read from the lanes' registers by permutes (every
@@ -848,20 +851,30 @@ __global__ __launch_bounds__(kBlock, kRolloutWavesPerSimd) void rollout_kernel(R
                     }
                 }
                 CoopWave& cw = coop[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];  // wave-uniform: an SGPR base
-                if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
-                    const u32 tbl = side == OTH_BLACK ? tbl_black : tbl_black ^ 1u;
-                    const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, cw, rays, w_s, kth_tab, (u32)lane,
-                                                      a.coop_cap);
-                    if (choose) sq = c;
-                }
-                if (moving) {
-                    if (RECORD) rec_put(ply, (uint8_t)sq);
-                    place(P, O, flips_rays(sq, run_sets(pos), rays));
+                auto play = [&](u32 m, const RunSets& rs) {
+                    if (RECORD) rec_put(ply, (uint8_t)m);
+                    place(P, O, flips_rays(m, rs, rays));
                     const u64 np = O;
                     O = P;
                     P = np;
                     side ^= 3u;
                     ply++;
+                };
+                // a move already decided (random) is played before the wave's
+                // choice; a chosen one after it, from the run sets the lane
+                // published to its LDS record (round 6: the position's run sets
+                // were live in VGPRs across every child of the choice)
+                if (moving && !choose) play(sq, run_sets(pos));
+                if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
+                    const u32 tbl = side == OTH_BLACK ? tbl_black : tbl_black ^ 1u;
+                    const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, cw, rays, w_s, kth_tab, (u32)lane,
+                                                      a.coop_cap);
+                    if (choose) {
+                        u64 Pr, Or;
+                        RunSets rs;
+                        load_parent(cw.rec[lane], Pr, Or, rs);
+                        play(c, rs);
+                    }
                 }
             }
         }

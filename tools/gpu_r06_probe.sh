@@ -19,7 +19,7 @@ import csv, glob, sys, collections, re
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"rollout_kernel<(\d), false>", r["Kernel_Name"])
+        m = re.search(r"rollout_kernel<(\d), false, false>", r["Kernel_Name"])
         if m:
             acc[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in sorted(acc.items()):

@@ -44,16 +44,40 @@ def short(name):
     return None
 
 
-def pmc(d):
+def pmc(d, durs=None):
+    """Counter values per (kernel, grid); with `durs`, also each dispatch's
+    duration in this pass (PMC passes serialize the dispatches, so this is a
+    launch alone on the chip), once per dispatch."""
     out = collections.defaultdict(lambda: collections.defaultdict(list))
+    seen = set()
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             if k is None:
                 continue
             # key by grid size too: step_kernel runs at two batch sizes
-            out[(k, int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            key = (k, int(r["Grid_Size"]))
+            out[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if durs is not None and (f, r["Dispatch_Id"]) not in seen and r.get("End_Timestamp"):
+                seen.add((f, r["Dispatch_Id"]))
+                durs[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return out
+
+
+PASSES = {
+    "avg_ns": "kernel-trace pass (rocprofv3 --kernel-trace --stats) of the bench command: launches as the bench "
+              "issues them, so the headline rollout shares the chip with the launch on the other stream "
+              "(two in flight)",
+    "avg_ns_serialized": "the GRBM PMC pass of the same command: counter collection serializes dispatches, so each "
+                         "launch runs alone on the chip",
+    "fetch_bytes_raw/fetch_bytes_corrected": "FETCH_SIZE pass (x2 gfx950 correction)",
+    "write_bytes": "WRITE_SIZE pass",
+    "SQ_*": "SQ pass (serialized dispatches)",
+    "GRBM_GUI_ACTIVE/gpu_cycles_pmc": "GRBM pass (serialized dispatches); gpu_cycles_pmc = GRBM_GUI_ACTIVE / 8 XCDs",
+    "clock_ghz_pmc": "gpu_cycles_pmc / avg_ns_serialized, both from the GRBM pass (one dispatch, one pass)",
+    "valu_issue_frac": "2 x SQ_INSTS_VALU (SQ pass) / (1024 SIMDs x gpu_cycles_pmc (GRBM pass)): both serialized; "
+                       "not comparable with avg_ns, which overlaps a neighbouring launch",
+}
 
 
 def main(d):
@@ -71,8 +95,9 @@ def main(d):
             if k:
                 trace[(k, int(r.get("Grid_Size") or r["Grid_Size_X"]))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     counters = {}
+    serialized = collections.defaultdict(list)
     for sub in ("fetch", "write", "sq", "grbm"):
-        for key, cs in pmc(os.path.join(d, sub)).items():
+        for key, cs in pmc(os.path.join(d, sub), serialized if sub == "grbm" else None).items():
             for c, v in cs.items():
                 counters.setdefault(key, {})[c] = sum(v) / len(v)
     # the build every figure below was measured on (bench.py compares it with
@@ -80,13 +105,16 @@ def main(d):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     from subproc_amd._lib import library_sha16
-    out = {"library_sha16": library_sha16(), "kernels": {}}
+    out = {"library_sha16": library_sha16(), "passes": PASSES, "kernels": {}}
     for (k, grid), cs in sorted(counters.items()):
         e = {"grid_threads": grid}
         durs = trace.get((k, grid))
         if durs:
             e["launches"] = len(durs)
             e["avg_ns"] = sum(durs) / len(durs)
+        sd = serialized.get((k, grid))
+        if sd:
+            e["avg_ns_serialized"] = sum(sd) / len(sd)
         if "FETCH_SIZE" in cs:
             e["fetch_bytes_raw"] = cs["FETCH_SIZE"] * 1024
             e["fetch_bytes_corrected"] = 2 * cs["FETCH_SIZE"] * 1024
@@ -101,6 +129,8 @@ def main(d):
             # GPU cycles of the (serialized) PMC dispatch; not divided by the kernel-trace
             # duration, which overlaps a neighbouring launch in the two-stream bench
             e["gpu_cycles_pmc"] = cs["GRBM_GUI_ACTIVE"] / 8
+            if e.get("avg_ns_serialized"):
+                e["clock_ghz_pmc"] = e["gpu_cycles_pmc"] / e["avg_ns_serialized"]
             if "SQ_INSTS_VALU" in cs and e["gpu_cycles_pmc"] > 0:
                 e["valu_issue_frac"] = 2 * cs["SQ_INSTS_VALU"] / (N_SIMD * e["gpu_cycles_pmc"])
         out["kernels"][f"{k}@{grid}"] = e

@@ -214,17 +214,18 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 template <int POLICY>
 __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos, CoopWave& cw, const u64* rays,
                            const int* w_s, const uint8_t* kth_tab, u32 lane, u32 cap) {
-    // the record is published first, on either path: the caller plays the
-    // chosen move from it (its run sets need not stay in VGPRs across the
-    // children, round 6)
-    if (need) {
+    auto publish = [&] {
         u64* r = cw.rec[lane];
         r[0] = P;
         r[1] = O;
         RunSets rs = run_sets(pos);  // reversed once per parent, not per child
         if (POLICY == OTH_POLICY_EVAL) rs.A1 |= (u64)(tbl & 1u);
         *reinterpret_cast<RunSets*>(r + 2) = rs;
-    }
+    };
+    // greedy (round 6): the record first, on either path, since the caller
+    // plays the chosen move from it
+    constexpr bool kFirst = POLICY == OTH_POLICY_GREEDY;
+    if (kFirst && need) publish();
     if (cap == 0) return need ? lane_choose<POLICY>(pos, P, O, rays, w_s + (tbl ? kEvalTable : 0)) : 64u;
     const u64 legal = need ? pos.legal : 0ull;
     const u32 cnt = (u32)__popcll(legal);
@@ -232,7 +233,10 @@ __device__ u32 coop_choose(bool need, u64 P, u64 O, u32 tbl, const Position& pos
     const u32 T = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     const u32 R = (T + 63u) >> 6;
     cw.legal[lane] = legal;
-    if (need) cw.best[lane] = 0xFFFFFFFFu;
+    if (need) {
+        if (!kFirst) publish();
+        cw.best[lane] = 0xFFFFFFFFu;
+    }
     // this lane's chunk of the children: [t0, t0 + cnt_mine).  Its first
     // parent, the last lane whose first child is <= t0, by a binary search of
     // the exclusive scan, read from the lanes' registers by permutes (every
@@ -586,11 +590,14 @@ constexpr size_t rec_stage_bytes(int policy, bool record) {
 // the random loop's fill order (bitboard.hpp analyse): with the VOP3 logic,
 // 7-8-9 leaves the fewest same-bank v_bitop3_b32 in its loop (tools/valu_mix.py)
 constexpr int kRandomFillOrder = 789;
-// every rollout kernel: >= 4 waves/SIMD, <= 128 VGPRs (greedy at 5, 96 VGPRs,
-// ran slower: profiles/r05_notes.md)
-constexpr int kRolloutWavesPerSimd = 4;
+// occupancy floor of the rollout kernels (launch bounds): random and eval
+// >= 4 waves/SIMD (<= 128 VGPRs); greedy 5 (<= 96 VGPRs; its spills are in the
+// ply loop, none in the child loop): two streams 3.200 -> 3.236e10 env-steps/s
+// with the record change above (round 5, before it: +1.0% at two streams, a
+// mixed result at one; profiles/r06_notes.md)
+constexpr int rollout_waves_per_simd(int policy) { return policy == OTH_POLICY_GREEDY ? 5 : 4; }
 template <int POLICY, bool RECORD, bool RUNNER = false>
-__global__ __launch_bounds__(kBlock, kRolloutWavesPerSimd) void rollout_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(kBlock, rollout_waves_per_simd(POLICY)) void rollout_kernel(RolloutArgs a) {
     __shared__ unsigned long long hist_s[OTH_HIST_BINS];
     __shared__ uint8_t kth_tab[256 * 8];
     __shared__ u64 rays[kTabRows * 64];
@@ -860,22 +867,31 @@ __global__ __launch_bounds__(kBlock, kRolloutWavesPerSimd) void rollout_kernel(R
                     side ^= 3u;
                     ply++;
                 };
-                // a move already decided (random) is played before the wave's
-                // choice; a chosen one after it, from the run sets the lane
-                // published to its LDS record (round 6: the position's run sets
-                // were live in VGPRs across every child of the choice)
-                if (moving && !choose) play(sq, run_sets(pos));
+                // Greedy (round 6): a move already decided (random) is played
+                // before the wave's choice, a chosen one after it from the run
+                // sets the lane published to its LDS record, so the position's
+                // run sets are not live in VGPRs across every child of the
+                // choice: greedy 2.152 -> 2.121 ms per 1M-game launch on one
+                // stream, and room for 5 waves per SIMD (below).  Eval keeps
+                // them in registers: the same change cost it 3.80 -> 3.97 ms
+                // (tools/gpu_greedy_ab.sh, profiles/r06_notes.md).
+                constexpr bool kFromRecord = POLICY == OTH_POLICY_GREEDY;
+                if (kFromRecord && moving && !choose) play(sq, run_sets(pos));
                 if (__ballot(choose)) {  // wave-uniform: every lane of the wave joins
                     const u32 tbl = side == OTH_BLACK ? tbl_black : tbl_black ^ 1u;
                     const u32 c = coop_choose<POLICY>(choose, P, O, tbl, pos, cw, rays, w_s, kth_tab, (u32)lane,
                                                       a.coop_cap);
                     if (choose) {
-                        u64 Pr, Or;
-                        RunSets rs;
-                        load_parent(cw.rec[lane], Pr, Or, rs);
-                        play(c, rs);
+                        sq = c;
+                        if (kFromRecord) {
+                            u64 Pr, Or;
+                            RunSets rs;
+                            load_parent(cw.rec[lane], Pr, Or, rs);
+                            play(c, rs);
+                        }
                     }
                 }
+                if (!kFromRecord && moving) play(sq, run_sets(pos));
             }
         }
         if constexpr (kRecStage) {  // the wave's records, one contiguous span, 16 bytes a lane

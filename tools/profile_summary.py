@@ -74,7 +74,9 @@ PASSES = {
     "write_bytes": "WRITE_SIZE pass",
     "SQ_*": "SQ pass (serialized dispatches)",
     "GRBM_GUI_ACTIVE/gpu_cycles_pmc": "GRBM pass (serialized dispatches); gpu_cycles_pmc = GRBM_GUI_ACTIVE / 8 XCDs",
-    "clock_ghz_pmc": "gpu_cycles_pmc / avg_ns_serialized, both from the GRBM pass (one dispatch, one pass)",
+    "clock_ghz_pmc": "gpu_cycles_pmc / avg_ns_serialized, both from the GRBM pass (one dispatch, one pass); "
+                     "meaningful for launches of >> 10 us only (a few-us launch's GRBM count includes the "
+                     "dispatch's fixed overhead outside its timestamps)",
     "valu_issue_frac": "2 x SQ_INSTS_VALU (SQ pass) / (1024 SIMDs x gpu_cycles_pmc (GRBM pass)): both serialized; "
                        "not comparable with avg_ns, which overlaps a neighbouring launch",
 }

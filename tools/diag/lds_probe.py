@@ -1,7 +1,8 @@
 """A short program for PMC passes (diagnostic, GPU box): 1,048,576-game
 rollouts of the random, greedy and eval policies (config 3 / config 5 / the
-eval player), two launches each on one stream, after one untimed launch each.
-    rocprofv3 --pmc <counters> -- python3 tools/diag/lds_probe.py"""
+eval player), three launches each on one stream, outputs written as the bench
+writes them (final boards, diff, plies).
+    rocprofv3 --pmc <counters> -- python3 tools/diag/lds_probe.py [policy,...]"""
 import os
 import sys
 
@@ -12,10 +13,9 @@ from subproc_amd import ops  # noqa: E402
 from subproc_amd.params import DEFAULT_WEIGHTS  # noqa: E402
 
 n = 1 << 20
-for pol in ("random", "greedy", "eval"):
+for pol in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("random", "greedy", "eval")):
     w = DEFAULT_WEIGHTS if pol == "eval" else None
     for k in range(3):
-        ops.rollout(n, 0x5EED, (k + 1) * n, pol, 10, device="cuda", weights=w, want_boards=False, want_diff=False,
-                    want_plies=False)
+        ops.rollout(n, 0x5EED, (k + 1) * n, pol, 10, device="cuda", weights=w)
     torch.cuda.synchronize()
     print(pol, "done", flush=True)

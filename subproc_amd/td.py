@@ -352,6 +352,10 @@ class StateMap:
                 # takes the count from the device (oth_td_lookup_dev), so the
                 # host's read below overlaps it (round 5: the read and the
                 # Python after it left the GPU idle ~50 us per batch)
+                # sized for every update, not the distinct keys (unknown yet):
+                # ~9 B per update, ~290 MB at a 32M-update batch, short-lived
+                # and recycled batch to batch by torch's caching allocator --
+                # the memory price of queuing the lookup early
                 n_max = ukeys.numel()
                 init = torch.empty(n_max, dtype=torch.float64, device=self.device)
                 is_new = torch.empty(n_max, dtype=torch.uint8, device=self.device)

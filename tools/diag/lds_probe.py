@@ -7,6 +7,9 @@ import os
 import sys
 
 sys.path.insert(0, os.getcwd())
+if os.environ.get("PROBE_LIB"):  # an A/B build instead of the in-tree library
+    from subproc_amd import _lib  # noqa: E402
+    _lib.LIB_PATH = os.path.abspath(os.environ["PROBE_LIB"])
 import torch  # noqa: E402
 
 from subproc_amd import ops  # noqa: E402

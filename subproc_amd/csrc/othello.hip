@@ -813,13 +813,21 @@ __global__ __launch_bounds__(kBlock, rollout_waves_per_simd(POLICY)) void rollou
                             // a full board needs no hand-over iteration to know it
                             const u64 bl = side == OTH_BLACK ? P : O, wh = side == OTH_BLACK ? O : P;
                             const int d = __popcll(bl) - __popcll(wh);
+                            // greedy (5 waves/SIMD, <= 96 VGPRs): the output
+                            // addresses computed here from an opaque copy of g,
+                            // and the game's plies into the block histogram
+                            // directly, so that neither is a register live
+                            // across the choice (hoisted, hipcc spilled them)
+                            u64 gt = g;
+                            if (POLICY == OTH_POLICY_GREEDY) asm volatile("" : "+v"(gt));
                             if (a.final_boards)
-                                reinterpret_cast<ulonglong2*>(a.final_boards)[g] = make_ulonglong2(bl, wh);
-                            if (a.diff) a.diff[g] = (int8_t)d;
-                            if (a.plies) a.plies[g] = (uint8_t)ply;
+                                reinterpret_cast<ulonglong2*>(a.final_boards)[gt] = make_ulonglong2(bl, wh);
+                            if (a.diff) a.diff[gt] = (int8_t)d;
+                            if (a.plies) a.plies[gt] = (uint8_t)ply;
                             atomicAdd(&hist_s[d + 64], 1ull);
                             atomicAdd(&hist_s[d > 0 ? 129 : (d < 0 ? 130 : 131)], 1ull);
-                            plies_sum += ply;
+                            if (POLICY == OTH_POLICY_GREEDY) atomicAdd(&hist_s[132], (unsigned long long)ply);
+                            else plies_sum += ply;
                             active = false;
                         } else {
                             // the mover must pass: hand the move over tentatively; the pass

@@ -50,7 +50,14 @@ def kernel_notes(tmp_path):
 # Measured (profiles/r05_notes.md): 3.810 ms per 1M-game launch against 3.945
 # ms rereading the record per child, and 3.883 ms at 3 waves/SIMD without the
 # spill.  Any other scratch, or more than this, fails.
-SCRATCH_ALLOWED = {"rollout_kernelILi2E": 32}
+# Round 6: the greedy kernels run at 5 waves per SIMD (<= 96 VGPRs), where hipcc
+# spills a few per-batch values (the game index, the RNG increment, the opening
+# boards; <= 68 B per lane, none in the child loop).  Measured against the
+# same code at 4 waves without scratch (profiles/r06_notes.md, tools/
+# gpu_greedy_ab.sh): 3.239e10 against 3.198e10 env-steps/s at two streams,
+# 2.116 against 2.140 ms per one-stream launch; the scratch adds 16.8 MB of
+# HBM writes per 1M-game launch (37.4 against 20.6 MB), 10 GB/s.
+SCRATCH_ALLOWED = {"rollout_kernelILi2E": 32, "rollout_kernelILi1E": 68}
 
 
 def test_no_kernel_uses_scratch(tmp_path):

@@ -167,12 +167,21 @@ def spawn_ranks(n, cmd, env=None, port=None, poll_s=0.2):
     base = dict(os.environ if env is None else env)
     port = port or free_port()
     procs = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(cmd, env=e, start_new_session=True))
+
+    def end_all(sig):  # the exact children this call started, never a pattern
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(sig)
+
+    # the children stay in this process's group, so a timeout that kills the
+    # group ends them too; a SIGTERM to this process alone is passed on
+    prev = signal.signal(signal.SIGTERM, lambda *_: (end_all(signal.SIGTERM), sys.exit(128 + signal.SIGTERM)))
     rc = 0
     try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                     MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(cmd, env=e))
         live = list(procs)
         while live:
             for p in list(live):
@@ -182,15 +191,14 @@ def spawn_ranks(n, cmd, env=None, port=None, poll_s=0.2):
                 live.remove(p)
                 if c != 0 and rc == 0:
                     rc = c if c > 0 else 128 - c
-                    for q in live:  # the exact children this call started
-                        os.killpg(q.pid, signal.SIGTERM)
+                    end_all(signal.SIGTERM)  # their collectives can no longer complete
             if live:
                 time.sleep(poll_s)
     finally:
+        end_all(signal.SIGKILL)
         for p in procs:
-            if p.poll() is None:
-                os.killpg(p.pid, signal.SIGKILL)
-                p.wait()
+            p.wait()
+        signal.signal(signal.SIGTERM, prev)
     return rc
 
 

@@ -53,3 +53,30 @@ def test_bench_gpus2_without_torchrun_fails_loudly_without_a_gpu():
                         "--no-secondary"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_sigterm_to_the_launcher_ends_its_ranks(tmp_path):
+    """A SIGTERM to the launcher (a driver's timeout) reaches the ranks: the
+    launcher exits 128 + 15 and no rank outlives it."""
+    import signal
+
+    child = ("import os, sys, time; open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write(str(os.getpid())); "
+             "time.sleep(120)")
+    prog = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.spawn_ranks(2, [sys.executable, '-c', %r, %r]))" % (ROOT, child, str(tmp_path)))
+    p = subprocess.Popen([sys.executable, "-c", prog])
+    t0 = time.time()
+    while len(os.listdir(tmp_path)) < 2 and time.time() - t0 < 60:
+        time.sleep(0.1)
+    pids = [int(open(tmp_path / f).read()) for f in os.listdir(tmp_path)]
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    time.sleep(0.5)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, pid

@@ -1024,8 +1024,14 @@ __device__ __forceinline__ void load_move_record(const uint8_t* row, bool vec, u
 constexpr int kReplayBursts = (OTH_POS_STRIDE + 7 + kReplayBurst - 1) / kReplayBurst;  // 17 for every alignment
 constexpr int kXHalf = kReplayBurst / 2;  // rows per exchange
 // the packed layout's stage: the block's bytes start at a 16-B chunk offset of
-// up to 15, and its turn / end ranges are chunked from there
-constexpr int kReplayStagePacked = kReplayStage + 16;
+// up to 15, and its turn / end ranges are chunked from there.  Sized for 72
+// rows per game (round 6; self-play games record 61-62 rows on average and
+// at most ~70), not the stride's 129: a block whose rows do not fit writes its
+// bytes directly (below).  With the 16 KiB row exchange that is 37 KiB of LDS
+// per block, so 4 blocks fit a CU, and the 4,096 waves of a 262,144-game launch
+// are resident at once instead of in one and a third rounds.
+constexpr int kReplayPackedRows = 72;
+constexpr int kReplayStagePacked = kBlock * kReplayPackedRows + 16;
 
 // Two output layouts (include/othello.h):
 //  * strided (PACKED = false): game i's position p at row i*OTH_POS_STRIDE + p,
@@ -1038,7 +1044,7 @@ constexpr int kReplayStagePacked = kReplayStage + 16;
 //    16-B chunk boundary; the chunks the range shares with the neighbouring
 //    blocks are written byte by byte.
 template <bool PACKED>
-__global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict__ start,
+__global__ __launch_bounds__(kBlock, PACKED ? 4 : 3) void replay_kernel(const u64* __restrict__ start,
                                                         const uint8_t* __restrict__ start_turn,
                                                         const uint8_t* __restrict__ moves,
                                                         const uint8_t* __restrict__ plies,
@@ -1140,13 +1146,18 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
         const int p0 = 8 * bi - s;
         // move codes p0 .. p0+7 (bytes before position 0 are never used)
         const u64 win = s ? (cur << (8 * s)) | (prev >> (64 - 8 * s)) : cur;
-        ulonglong2 b[kReplayBurst];
+        // each half's 4 rows go straight into the wave's LDS exchange as they
+        // are built (round 6: an 8-row register buffer held 32 more VGPRs)
 #pragma unroll
-        for (int k = 0; k < kReplayBurst; k++) {
+        for (int h = 0; h < kReplayBurst / kXHalf; h++) {
+          u32 valid = 0;
+#pragma unroll
+          for (int kk = 0; kk < kXHalf; kk++) {
+            const int k = h * kXHalf + kk;
             const int p = p0 + k;
-            b[k] = make_ulonglong2(0ull, 0ull);  // rows past plies are 0
+            ulonglong2 row = make_ulonglong2(0ull, 0ull);  // rows past plies are 0
             if (p >= 0 && p <= np) {
-                b[k] = make_ulonglong2(bl, wh);
+                row = make_ulonglong2(bl, wh);
                 const u32 c = (u32)(win >> (8 * k)) & 0xffu;
                 const bool fast = t == OTH_BLACK || t == OTH_WHITE;
                 if (pos_end && fast) {
@@ -1173,8 +1184,7 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                     } else if (p < np && c == OTH_PASS) {
                         t ^= 3u;
                     }
-                    continue;
-                }
+                } else {
                 if (staged) {
                     u32 e = 0;
                     if (pos_end && moves_of(bl, wh) == 0) e = moves_of(wh, bl) == 0;
@@ -1205,18 +1215,11 @@ __global__ __launch_bounds__(kBlock, 3) void replay_kernel(const u64* __restrict
                         }
                     }
                 }
+                }
             }
-        }
-#pragma unroll
-        for (int h = 0; h < kReplayBurst / kXHalf; h++) {
-            u32 valid = 0;
-#pragma unroll
-            for (int k = 0; k < kXHalf; k++) {
-                const int p = p0 + h * kXHalf + k;
-                const ulonglong2 v = b[h * kXHalf + k];
-                xrow[lane * kXHalf + k] = make_uint4((u32)v.x, (u32)(v.x >> 32), (u32)v.y, (u32)(v.y >> 32));
-                valid |= (live && p >= 0 && p < (PACKED ? np + 1 : OTH_POS_STRIDE) ? 1u : 0u) << k;
-            }
+            xrow[lane * kXHalf + kk] = make_uint4((u32)row.x, (u32)(row.x >> 32), (u32)row.y, (u32)(row.y >> 32));
+            valid |= (live && p >= 0 && p < (PACKED ? np + 1 : OTH_POS_STRIDE) ? 1u : 0u) << kk;
+          }
             xaddr[lane] = reinterpret_cast<unsigned long long>(out + (p0 + h * kXHalf));
             xmask[lane] = valid;
             wave_sync();

@@ -1142,12 +1142,6 @@ __global__ __launch_bounds__(kBlock, PACKED ? 4 : 3) void replay_kernel(const u6
         for (int off = 32; off >= 1; off >>= 1) bursts = max(bursts, __shfl_xor(bursts, off));
     }
     u64 prev = 0, cur = R[0];   // move-record words w[b-1], w[b] of burst b
-    // the game's final position (p == np), whose is_game_over is taken once
-    // after the bursts for the whole wave (round 6): inside them the wave ran
-    // the two analyses at every position where any of its 64 games ended
-    u64 fin_bl = 0, fin_wh = 0;
-    u32 fin_t = 0;
-    bool fin = false;
     for (int bi = 0; bi < bursts; bi++) {
         const int p0 = 8 * bi - s;
         // move codes p0 .. p0+7 (bytes before position 0 are never used)
@@ -1179,14 +1173,7 @@ __global__ __launch_bounds__(kBlock, PACKED ? 4 : 3) void replay_kernel(const u6
                     u64 f = 0;
                     if (p < np && c < 64 && !((P | O) >> c & 1ull)) f = flips_carry(c, P, O);
                     u32 e = 0;
-                    if (p == np) {  // deferred (above); its byte is rewritten after the bursts
-                        fin = true;
-                        fin_bl = bl;
-                        fin_wh = wh;
-                        fin_t = t;
-                    } else if (!f && moves_of(P, O) == 0) {
-                        e = moves_of(O, P) == 0;
-                    }
+                    if (!f && moves_of(P, O) == 0) e = moves_of(O, P) == 0;
                     put_te(p, t | (e << 7), t);
                     if (f) {
                         P = or3(P, f, 1ull << c);
@@ -1249,12 +1236,6 @@ __global__ __launch_bounds__(kBlock, PACKED ? 4 : 3) void replay_kernel(const u6
         for (int j = 0; j < OTH_MOVES_STRIDE / 8 - 1; j++) R[j] = R[j + 1];
         R[OTH_MOVES_STRIDE / 8 - 1] = 0;
         cur = R[0];
-    }
-    if (fin) {  // every finished lane's final position at once: one pass of the wave
-        const bool black = fin_t == OTH_BLACK;
-        const u64 P = black ? fin_bl : fin_wh, O = black ? fin_wh : fin_bl;
-        const u32 e = moves_of(P, O) == 0 && moves_of(O, P) == 0;
-        put_te(np, fin_t | (e << 7), fin_t);
     }
     if (!staged || direct) return;
     __syncthreads();

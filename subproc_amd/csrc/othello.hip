@@ -591,10 +591,11 @@ constexpr size_t rec_stage_bytes(int policy, bool record) {
 // 7-8-9 leaves the fewest same-bank v_bitop3_b32 in its loop (tools/valu_mix.py)
 constexpr int kRandomFillOrder = 789;
 // occupancy floor of the rollout kernels (launch bounds): random and eval
-// >= 4 waves/SIMD (<= 128 VGPRs); greedy 5 (<= 96 VGPRs; its spills are in the
-// ply loop, none in the child loop): two streams 3.200 -> 3.236e10 env-steps/s
-// with the record change above (round 5, before it: +1.0% at two streams, a
-// mixed result at one; profiles/r06_notes.md)
+// >= 4 waves/SIMD (<= 128 VGPRs); greedy 5 (<= 96 VGPRs; hipcc spills 13
+// per-batch registers, none in the child loop): with the record change above,
+// two streams 3.198 -> 3.24e10 env-steps/s and one stream 2.140 -> 2.116 ms
+// per 1M-game launch against 4 waves (profiles/r06_notes.md §10; round 5,
+// before the record change: +1.0% at two streams, a mixed result at one)
 constexpr int rollout_waves_per_simd(int policy) { return policy == OTH_POLICY_GREEDY ? 5 : 4; }
 template <int POLICY, bool RECORD, bool RUNNER = false>
 __global__ __launch_bounds__(kBlock, rollout_waves_per_simd(POLICY)) void rollout_kernel(RolloutArgs a) {
